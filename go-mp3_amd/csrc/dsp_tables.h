@@ -1,0 +1,46 @@
+// dsp_tables.h -- constant tables of the granule DSP, computed on the host
+// exactly as the reference initialises them, then uploaded once per device.
+//
+// Reference initialisers:
+//   synthNWin      internal/frame/frame.go:488-497
+//   synthDtbl      internal/frame/frame.go:499-628   (ISO 11172-3 Table B.3)
+//   imdctWinData   internal/imdct/imdct.go:21-57
+//   cosN12/cosN36  internal/imdct/imdct.go:59-79
+//   powtab34       internal/frame/frame.go:31-40
+//   isRatios       internal/frame/frame.go:304-306
+//   cs/ca          internal/frame/frame.go:422-425
+//   SfBandIndices  internal/consts/consts.go:68-97
+#pragma once
+#include <cstdint>
+
+namespace mp3g {
+
+// Line tables per (lsf, sampling-frequency index) combination: combo = lsf*3 + sfreq.
+constexpr int kCombos = 6;
+
+struct DspTables {
+  // Requantization: req[r][a] = float32(pow(2, r/4) * powtab34[a]), r = 0..3,
+  // a = 0..8206.  float32(pow(2, n/4) * powtab34[a]) == ldexp(req[n&3][a], n>>2)
+  // for every n the bitstream can produce (tests/test_tables.py proves it
+  // exhaustively against the oracle's direct float64 evaluation).
+  float req[4][8207];
+  float nwin[64][32];
+  float synth_d[512];
+  float imdct_win[4][36];
+  float cos12[6][12];
+  float cos36[18][36];
+  float is_ratio[7][2];     // [is_pos][ch]: f32 ratios as stereoProcessIntensity* computes them
+  float aa_cs[8], aa_ca[8];
+  uint16_t sfb_long[kCombos][23];
+  uint16_t sfb_short[kCombos][14];
+  uint8_t line_long_sfb[kCombos][576];   // long scale-factor band of line i
+  // short-block info of line i in source (window-major) order:
+  //   bits 0..3 short sfb, bits 4..5 window, bits 6..15 reordered destination
+  uint16_t line_short[kCombos][576];
+  int8_t pretab[22];
+};
+
+// Fills `t` (deterministic, thread-safe).
+void build_tables(DspTables* t);
+
+}  // namespace mp3g

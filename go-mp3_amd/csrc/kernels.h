@@ -1,0 +1,34 @@
+// kernels.h -- device-side work descriptors and kernel entry points.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../../include/mp3g.h"
+#include "dsp_tables.h"
+
+namespace mp3g {
+
+constexpr uint32_t kChunkStateIn = 1u;   // stream starts from state_in[stream]
+constexpr uint32_t kChunkStateOut = 2u;  // this chunk ends its stream and exports state
+
+// One workgroup's work: decode granules [out_first, out_first + n_out) of the
+// stream that starts at stream_first (32 bytes).
+struct ChunkDesc {
+  uint64_t out_first;
+  uint64_t stream_first;
+  uint32_t n_out;
+  uint32_t stream;
+  uint32_t flags;
+  uint32_t reserved;
+};
+static_assert(sizeof(ChunkDesc) == 32, "ChunkDesc layout");
+
+// Host-side launchers (defined next to the kernels; no RDC needed).
+hipError_t upload_tables(const DspTables& tables);
+hipError_t launch_granule_exact(const ChunkDesc* d_chunks, uint32_t n_chunks,
+                                const mp3g_granule* d_gran, const int16_t* d_coef,
+                                const mp3g_state* d_state_in, mp3g_state* d_state_out,
+                                int16_t* d_pcm, hipStream_t stream);
+
+}  // namespace mp3g

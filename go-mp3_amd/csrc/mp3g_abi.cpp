@@ -1,0 +1,336 @@
+// mp3g_abi.cpp -- C-ABI of libmp3g.so (declared in include/mp3g.h).
+//
+// Host side of the drop-in boundary for Frame.Decode (reference
+// internal/frame/frame.go:121).  No exception crosses the ABI; every entry
+// returns an mp3g_status.  The caller's current HIP device is restored on
+// return, so a host framework sharing the process (PyTorch) is unaffected.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/mp3g.h"
+#include "dsp_tables.h"
+#include "kernels.h"
+
+using namespace mp3g;
+
+namespace {
+
+thread_local std::string t_last_error;
+
+int fail(int status, const char* what, hipError_t e = hipSuccess) {
+  t_last_error = what;
+  if (e != hipSuccess) {
+    t_last_error += ": ";
+    t_last_error += hipGetErrorString(e);
+  }
+  return status;
+}
+
+#define HIP_TRY(expr)                                                   \
+  do {                                                                  \
+    hipError_t e_ = (expr);                                             \
+    if (e_ != hipSuccess) return fail(MP3G_ERR_DEVICE, #expr, e_);      \
+  } while (0)
+
+// Restores the caller's current device on scope exit.
+struct DeviceGuard {
+  int prev = -1;
+  hipError_t err = hipSuccess;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) err = hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+constexpr int kMaxDevices = 64;
+std::once_flag g_host_tables_once;
+DspTables* g_host_tables = nullptr;
+std::mutex g_dev_mu;
+bool g_dev_ready[kMaxDevices] = {};
+
+const DspTables& host_tables() {
+  std::call_once(g_host_tables_once, [] {
+    g_host_tables = new DspTables;
+    build_tables(g_host_tables);
+  });
+  return *g_host_tables;
+}
+
+// Uploads the constant tables to `dev` once.  Caller holds a DeviceGuard(dev).
+int ensure_device(int dev) {
+  if (dev < 0 || dev >= kMaxDevices) return fail(MP3G_ERR_INVALID_ARGUMENT, "device index");
+  std::lock_guard<std::mutex> lk(g_dev_mu);
+  if (g_dev_ready[dev]) return MP3G_OK;
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, dev));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(MP3G_ERR_NO_DEVICE, "device is not gfx950");
+  HIP_TRY(upload_tables(host_tables()));
+  HIP_TRY(hipDeviceSynchronize());
+  g_dev_ready[dev] = true;
+  return MP3G_OK;
+}
+
+}  // namespace
+
+struct mp3g_plan {
+  int device = 0;
+  uint32_t mode = 0;
+  uint32_t n_streams = 0;
+  std::vector<ChunkDesc> chunks;
+  ChunkDesc* d_chunks = nullptr;
+  uint64_t n_granules = 0;
+  uint64_t n_halo = 0;
+};
+
+extern "C" {
+
+int mp3g_abi_version(void) { return MP3G_ABI_VERSION; }
+
+const char* mp3g_status_string(int s) {
+  switch (s) {
+    case MP3G_OK: return "ok";
+    case MP3G_ERR_INVALID_ARGUMENT: return "invalid argument";
+    case MP3G_ERR_INVALID_GRANULE: return "invalid granule descriptor";
+    case MP3G_ERR_NO_DEVICE: return "no gfx950 device";
+    case MP3G_ERR_DEVICE: return "HIP runtime error";
+    case MP3G_ERR_OUT_OF_MEMORY: return "out of memory";
+    case MP3G_ERR_PARSE: return "bitstream parse error";
+    case MP3G_EOF: return "end of stream";
+    case MP3G_ERR_UNSUPPORTED: return "unsupported stream";
+  }
+  return "unknown status";
+}
+
+const char* mp3g_last_error(void) { return t_last_error.c_str(); }
+
+int mp3g_device_count(int* out_count) {
+  if (!out_count) return fail(MP3G_ERR_INVALID_ARGUMENT, "null out_count");
+  *out_count = 0;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return MP3G_OK;
+  int k = 0;
+  for (int d = 0; d < n; d++) {
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, d) == hipSuccess && std::strncmp(p.gcnArchName, "gfx950", 6) == 0) k++;
+  }
+  *out_count = k;
+  return MP3G_OK;
+}
+
+// Range checks of everything the DSP reads (what the reference bitstream
+// parse can produce); MPEG-2 mixed blocks are rejected because the reference
+// panics on them (maindata.go:139-178).
+int mp3g_validate(const mp3g_granule* g, const int16_t* coef, uint64_t n, uint64_t* bad) {
+  if (bad) *bad = 0;
+  if (n && (!g || !coef)) return fail(MP3G_ERR_INVALID_ARGUMENT, "null granules/coeffs");
+  for (uint64_t k = 0; k < n; k++) {
+    const uint32_t h = g[k].header;
+    bool ok = (h & 0xffe00000u) == 0xffe00000u;
+    const uint32_t id = (h >> 19) & 3u;
+    ok = ok && id != 1 && id != 0;             // reserved / MPEG 2.5 (frame.go:79-81)
+    ok = ok && ((h >> 17) & 3u) == 1u;         // layer III
+    ok = ok && ((h >> 12) & 15u) != 15u && ((h >> 12) & 15u) != 0u;
+    ok = ok && ((h >> 10) & 3u) != 3u;
+    const int nch = ((h >> 6) & 3u) == 3u ? 1 : 2;
+    const bool lsf = id != 3;
+    for (int ch = 0; ok && ch < nch; ch++) {
+      const mp3g_channel& c = g[k].ch[ch];
+      ok = c.count1 <= 576 && c.scalefac_scale <= 1 && c.preflag <= 1 && c.win_switch_flag <= 1 &&
+           c.block_type <= 3 && c.mixed_block_flag <= 1;
+      if (ok && !c.win_switch_flag) ok = c.block_type == 0 && c.mixed_block_flag == 0;
+      if (ok && lsf && c.block_type == 2 && c.mixed_block_flag) ok = false;
+      for (int w = 0; ok && w < 3; w++) ok = c.subblock_gain[w] <= 7;
+      for (int s = 0; ok && s < 22; s++) ok = c.scalefac_l[s] <= 15;
+      for (int s = 0; ok && s < 13; s++)
+        for (int w = 0; ok && w < 3; w++) ok = c.scalefac_s[s][w] <= 15;
+      const int16_t* x = coef + k * MP3G_COEF_PER_GRANULE + ch * MP3G_LINES;
+      for (int i = 0; ok && i < MP3G_LINES; i++) {
+        ok = x[i] <= 8206 && x[i] >= -8206;
+        if (ok && i >= c.count1) ok = x[i] == 0;  // zero region (maindata/huffman.go:130-134)
+      }
+    }
+    if (!ok) {
+      if (bad) *bad = k;
+      return fail(MP3G_ERR_INVALID_GRANULE, "granule descriptor out of range");
+    }
+  }
+  return MP3G_OK;
+}
+
+int mp3g_plan_create(int device, const mp3g_stream* streams, uint32_t n_streams,
+                     uint32_t granules_per_chunk, uint32_t mode, mp3g_plan** out_plan) {
+  if (!out_plan || (n_streams && !streams)) return fail(MP3G_ERR_INVALID_ARGUMENT, "null argument");
+  *out_plan = nullptr;
+  if ((mode & 0xffu) != MP3G_MODE_EXACT) return fail(MP3G_ERR_UNSUPPORTED, "mode not available");
+  uint64_t total = 0;
+  for (uint32_t s = 0; s < n_streams; s++) total += streams[s].n_granules;
+  uint32_t k = granules_per_chunk;
+  if (k == 0) {  // automatic: ~2048 workgroups, never fewer than 8 granules each
+    const uint64_t want = (total + 2047) / 2048;
+    k = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(want, 8), 1u << 20);
+  }
+  DeviceGuard guard(device);
+  if (guard.err != hipSuccess) return fail(MP3G_ERR_NO_DEVICE, "hipSetDevice", guard.err);
+  int st = ensure_device(device);
+  if (st) return st;
+  mp3g_plan* p = new (std::nothrow) mp3g_plan;
+  if (!p) return fail(MP3G_ERR_OUT_OF_MEMORY, "plan");
+  p->device = device;
+  p->mode = mode;
+  p->n_streams = n_streams;
+  for (uint32_t s = 0; s < n_streams; s++) {
+    const mp3g_stream& S = streams[s];
+    for (uint64_t off = 0; off < S.n_granules; off += k) {
+      ChunkDesc c{};
+      c.out_first = S.first_granule + off;
+      c.stream_first = S.first_granule;
+      c.n_out = (uint32_t)std::min<uint64_t>(k, S.n_granules - off);
+      c.stream = s;
+      c.flags = (S.flags & MP3G_STREAM_STATE_IN) ? kChunkStateIn : 0u;
+      if ((S.flags & MP3G_STREAM_STATE_OUT) && off + c.n_out == S.n_granules) c.flags |= kChunkStateOut;
+      p->chunks.push_back(c);
+      p->n_granules += c.n_out;
+      p->n_halo += std::min<uint64_t>(off, 2);
+    }
+    if (S.n_granules == 0 && (S.flags & MP3G_STREAM_STATE_OUT)) {
+      // empty stream exporting state: state_out = state_in (or zero)
+      ChunkDesc c{};
+      c.out_first = S.first_granule;
+      c.stream_first = S.first_granule;
+      c.n_out = 0;
+      c.stream = s;
+      c.flags = kChunkStateOut | ((S.flags & MP3G_STREAM_STATE_IN) ? kChunkStateIn : 0u);
+      p->chunks.push_back(c);
+    }
+  }
+  if (!p->chunks.empty()) {
+    hipError_t e = hipMalloc(&p->d_chunks, p->chunks.size() * sizeof(ChunkDesc));
+    if (e != hipSuccess) {
+      delete p;
+      return fail(MP3G_ERR_OUT_OF_MEMORY, "hipMalloc(chunks)", e);
+    }
+    e = hipMemcpy(p->d_chunks, p->chunks.data(), p->chunks.size() * sizeof(ChunkDesc),
+                  hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      (void)hipFree(p->d_chunks);
+      delete p;
+      return fail(MP3G_ERR_DEVICE, "hipMemcpy(chunks)", e);
+    }
+  }
+  *out_plan = p;
+  return MP3G_OK;
+}
+
+int mp3g_plan_destroy(mp3g_plan* p) {
+  if (!p) return MP3G_OK;
+  if (p->d_chunks) {
+    DeviceGuard guard(p->device);
+    (void)hipFree(p->d_chunks);
+  }
+  delete p;
+  return MP3G_OK;
+}
+
+int mp3g_plan_info(const mp3g_plan* p, uint64_t* n_chunks, uint64_t* n_granules, uint64_t* n_halo) {
+  if (!p) return fail(MP3G_ERR_INVALID_ARGUMENT, "null plan");
+  if (n_chunks) *n_chunks = p->chunks.size();
+  if (n_granules) *n_granules = p->n_granules;
+  if (n_halo) *n_halo = p->n_halo;
+  return MP3G_OK;
+}
+
+int mp3g_plan_execute(mp3g_plan* p, const mp3g_granule* d_gran, const int16_t* d_coef,
+                      const mp3g_state* d_state_in, mp3g_state* d_state_out, int16_t* d_pcm,
+                      void* hip_stream) {
+  if (!p) return fail(MP3G_ERR_INVALID_ARGUMENT, "null plan");
+  if (p->chunks.empty()) return MP3G_OK;
+  if (!d_gran || !d_coef || !d_pcm) return fail(MP3G_ERR_INVALID_ARGUMENT, "null device buffer");
+  DeviceGuard guard(p->device);
+  if (guard.err != hipSuccess) return fail(MP3G_ERR_NO_DEVICE, "hipSetDevice", guard.err);
+  for (const ChunkDesc& c : p->chunks) {
+    if ((c.flags & kChunkStateOut) && !d_state_out) return fail(MP3G_ERR_INVALID_ARGUMENT, "state_out needed");
+  }
+  HIP_TRY(launch_granule_exact(p->d_chunks, (uint32_t)p->chunks.size(), d_gran, d_coef, d_state_in,
+                               d_state_out, d_pcm, static_cast<hipStream_t>(hip_stream)));
+  return MP3G_OK;
+}
+
+int mp3g_decode_host(int device, const mp3g_granule* granules, const int16_t* coeffs,
+                     uint64_t n_granules, const mp3g_stream* streams, uint32_t n_streams,
+                     const mp3g_state* state_in, mp3g_state* state_out, int16_t* pcm,
+                     uint32_t mode) {
+  if (n_granules && (!granules || !coeffs || !pcm)) return fail(MP3G_ERR_INVALID_ARGUMENT, "null buffer");
+  bool need_in = false, need_out = false;
+  for (uint32_t s = 0; s < n_streams; s++) {
+    if (streams[s].first_granule + streams[s].n_granules > n_granules)
+      return fail(MP3G_ERR_INVALID_ARGUMENT, "stream exceeds granule array");
+    need_in |= (streams[s].flags & MP3G_STREAM_STATE_IN) != 0;
+    need_out |= (streams[s].flags & MP3G_STREAM_STATE_OUT) != 0;
+  }
+  if ((need_in && !state_in) || (need_out && !state_out))
+    return fail(MP3G_ERR_INVALID_ARGUMENT, "state buffer missing");
+  if (mode & MP3G_FLAG_CHECKED) {
+    int st = mp3g_validate(granules, coeffs, n_granules, nullptr);
+    if (st) return st;
+  }
+  mp3g_plan* plan = nullptr;
+  int st = mp3g_plan_create(device, streams, n_streams, 0, mode & 0xffu, &plan);
+  if (st) return st;
+  DeviceGuard guard(device);
+  void *dg = nullptr, *dc = nullptr, *dsi = nullptr, *dso = nullptr, *dp = nullptr;
+  hipStream_t stream = nullptr;
+  auto cleanup = [&]() {
+    if (stream) (void)hipStreamDestroy(stream);
+    for (void* q : {dg, dc, dsi, dso, dp})
+      if (q) (void)hipFree(q);
+    mp3g_plan_destroy(plan);
+  };
+  const size_t gb = n_granules * sizeof(mp3g_granule), cb = n_granules * MP3G_COEF_PER_GRANULE * 2,
+               pb = n_granules * MP3G_PCM_BYTES_PER_GRANULE, sb = n_streams * sizeof(mp3g_state);
+  hipError_t e = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking);
+  if (e == hipSuccess && gb) e = hipMalloc(&dg, gb);
+  if (e == hipSuccess && cb) e = hipMalloc(&dc, cb);
+  if (e == hipSuccess && pb) e = hipMalloc(&dp, pb);
+  if (e == hipSuccess && need_in) e = hipMalloc(&dsi, sb);
+  if (e == hipSuccess && need_out) e = hipMalloc(&dso, sb);
+  if (e != hipSuccess) {
+    cleanup();
+    return fail(MP3G_ERR_OUT_OF_MEMORY, "hipMalloc", e);
+  }
+  if (gb) e = hipMemcpyAsync(dg, granules, gb, hipMemcpyHostToDevice, stream);
+  if (e == hipSuccess && cb) e = hipMemcpyAsync(dc, coeffs, cb, hipMemcpyHostToDevice, stream);
+  if (e == hipSuccess && need_in) e = hipMemcpyAsync(dsi, state_in, sb, hipMemcpyHostToDevice, stream);
+  // streams without MP3G_STREAM_STATE_OUT keep the caller's state_out bytes
+  if (e == hipSuccess && need_out) e = hipMemcpyAsync(dso, state_out, sb, hipMemcpyHostToDevice, stream);
+  if (e != hipSuccess) {
+    cleanup();
+    return fail(MP3G_ERR_DEVICE, "hipMemcpyAsync(H2D)", e);
+  }
+  st = mp3g_plan_execute(plan, (const mp3g_granule*)dg, (const int16_t*)dc, (const mp3g_state*)dsi,
+                         (mp3g_state*)dso, (int16_t*)dp, stream);
+  if (st) {
+    cleanup();
+    return st;
+  }
+  if (pb) e = hipMemcpyAsync(pcm, dp, pb, hipMemcpyDeviceToHost, stream);
+  if (e == hipSuccess && need_out) e = hipMemcpyAsync(state_out, dso, sb, hipMemcpyDeviceToHost, stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(stream);
+  cleanup();
+  if (e != hipSuccess) return fail(MP3G_ERR_DEVICE, "decode", e);
+  return MP3G_OK;
+}
+
+}  // extern "C"

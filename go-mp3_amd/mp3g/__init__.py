@@ -1,0 +1,167 @@
+"""mp3g -- Python binding of libmp3g.so (the MI355X granule-decode C-ABI).
+
+The C-ABI (include/mp3g.h) is the product boundary; this module is a thin
+ctypes layer used by the tests and bench.py.  It never falls back to a CPU
+implementation: if libmp3g.so is missing or no gfx950 device is present the
+calls raise.
+
+Boundary structs mirror include/mp3g.h exactly (asserted sizes below).
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+__all__ = ["CHANNEL_DTYPE", "GRANULE_DTYPE", "STREAM_DTYPE", "STATE_DTYPE", "MODE_EXACT",
+           "MODE_FAST", "FLAG_CHECKED", "STATE_IN", "STATE_OUT", "Mp3gError", "lib", "lib_path",
+           "decode_host", "validate", "Plan", "device_count", "streams_for"]
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+CHANNEL_DTYPE = np.dtype([
+    ("count1", "<u2"), ("global_gain", "u1"), ("scalefac_scale", "u1"), ("preflag", "u1"),
+    ("win_switch_flag", "u1"), ("block_type", "u1"), ("mixed_block_flag", "u1"),
+    ("subblock_gain", "u1", (3,)), ("scalefac_l", "u1", (22,)), ("scalefac_s", "u1", (13, 3)),
+])
+GRANULE_DTYPE = np.dtype([("header", "<u4"), ("gr", "<u4"), ("ch", CHANNEL_DTYPE, (2,)),
+                          ("reserved", "u1", (8,))])
+STREAM_DTYPE = np.dtype([("first_granule", "<u8"), ("n_granules", "<u4"), ("flags", "<u4")])
+STATE_DTYPE = np.dtype([("store", "<f4", (2, 32, 18)), ("vvec", "<f4", (2, 1024))])
+assert CHANNEL_DTYPE.itemsize == 72 and GRANULE_DTYPE.itemsize == 160
+assert STREAM_DTYPE.itemsize == 16 and STATE_DTYPE.itemsize == 12800
+
+MODE_EXACT, MODE_FAST, FLAG_CHECKED = 0, 1, 0x100
+STATE_IN, STATE_OUT = 1, 2
+STATUS = {0: "ok", 1: "invalid argument", 2: "invalid granule", 3: "no device", 4: "device error",
+          5: "out of memory", 6: "parse error", 7: "eof", 8: "unsupported"}
+
+
+class Mp3gError(RuntimeError):
+    def __init__(self, status, msg=""):
+        super().__init__(f"mp3g status {status} ({STATUS.get(status, '?')}): {msg}")
+        self.status = status
+
+
+_lib = None
+
+
+def lib_path():
+    return os.path.join(HERE, "libmp3g.so")
+
+
+def lib():
+    """Load libmp3g.so (import torch first when sharing the process with it)."""
+    global _lib
+    if _lib is None:
+        path = lib_path()
+        if not os.path.exists(path):
+            raise Mp3gError(3, f"{path} not built (run __graft_entry__.build())")
+        L = C.CDLL(path)
+        vp, u32, u64 = C.c_void_p, C.c_uint32, C.c_uint64
+        L.mp3g_abi_version.restype = C.c_int
+        L.mp3g_status_string.argtypes = [C.c_int]
+        L.mp3g_status_string.restype = C.c_char_p
+        L.mp3g_last_error.restype = C.c_char_p
+        L.mp3g_device_count.argtypes = [C.POINTER(C.c_int)]
+        L.mp3g_validate.argtypes = [vp, vp, u64, C.POINTER(u64)]
+        L.mp3g_plan_create.argtypes = [C.c_int, vp, u32, u32, u32, C.POINTER(vp)]
+        L.mp3g_plan_destroy.argtypes = [vp]
+        L.mp3g_plan_info.argtypes = [vp, C.POINTER(u64), C.POINTER(u64), C.POINTER(u64)]
+        L.mp3g_plan_execute.argtypes = [vp, vp, vp, vp, vp, vp, vp]
+        L.mp3g_decode_host.argtypes = [C.c_int, vp, vp, u64, vp, u32, vp, vp, vp, u32]
+        _lib = L
+    return _lib
+
+
+def _check(st):
+    if st != 0:
+        raise Mp3gError(st, lib().mp3g_last_error().decode())
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def device_count():
+    n = C.c_int()
+    _check(lib().mp3g_device_count(C.byref(n)))
+    return n.value
+
+
+def streams_for(lengths, flags=0):
+    """Stream table for consecutive runs of granules with the given lengths."""
+    lengths = np.asarray(lengths, dtype=np.int64)
+    s = np.zeros(len(lengths), STREAM_DTYPE)
+    s["first_granule"] = np.concatenate([[0], np.cumsum(lengths)[:-1]]) if len(lengths) else []
+    s["n_granules"] = lengths
+    s["flags"] = flags
+    return s
+
+
+def validate(granules, coeffs):
+    granules = np.ascontiguousarray(granules, dtype=GRANULE_DTYPE)
+    coeffs = np.ascontiguousarray(coeffs, dtype=np.int16)
+    bad = C.c_uint64()
+    st = lib().mp3g_validate(_ptr(granules), _ptr(coeffs), len(granules), C.byref(bad))
+    return st, bad.value
+
+
+def decode_host(granules, coeffs, streams=None, state_in=None, state_out=None, mode=MODE_EXACT,
+                device=0):
+    """Synchronous decode of host arrays (the cgo drop-in entry, mp3g_decode_host).
+
+    granules: GRANULE_DTYPE[n]; coeffs: int16[n, 2, 576]; streams: STREAM_DTYPE[s]
+    (default: one stream covering everything).  Returns (pcm int16[n, 576, 2], state_out).
+    """
+    granules = np.ascontiguousarray(granules, dtype=GRANULE_DTYPE)
+    coeffs = np.ascontiguousarray(coeffs, dtype=np.int16)
+    n = len(granules)
+    assert coeffs.shape == (n, 2, 576), coeffs.shape
+    if streams is None:
+        streams = streams_for([n])
+    streams = np.ascontiguousarray(streams, dtype=STREAM_DTYPE)
+    if state_in is not None:
+        state_in = np.ascontiguousarray(state_in, dtype=STATE_DTYPE)
+    if state_out is None:
+        state_out = np.zeros(len(streams), STATE_DTYPE)
+    pcm = np.zeros((n, 576, 2), np.int16)
+    _check(lib().mp3g_decode_host(device, _ptr(granules), _ptr(coeffs), n, _ptr(streams),
+                                  len(streams), _ptr(state_in), _ptr(state_out), _ptr(pcm), mode))
+    return pcm, state_out
+
+
+class Plan:
+    """Device-resident plan (mp3g_plan_*): execute on device pointers / torch tensors."""
+
+    def __init__(self, streams, granules_per_chunk=0, mode=MODE_EXACT, device=0):
+        streams = np.ascontiguousarray(streams, dtype=STREAM_DTYPE)
+        self._h = C.c_void_p()
+        self.device = device
+        _check(lib().mp3g_plan_create(device, _ptr(streams), len(streams), granules_per_chunk,
+                                      mode, C.byref(self._h)))
+
+    def info(self):
+        a, b, c = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        _check(lib().mp3g_plan_info(self._h, C.byref(a), C.byref(b), C.byref(c)))
+        return {"chunks": a.value, "granules": b.value, "halo_granules": c.value}
+
+    def execute(self, d_gran, d_coef, d_pcm, d_state_in=None, d_state_out=None, stream=None):
+        """Pointers are ints (device addresses) or torch tensors; stream: hipStream_t int."""
+        def p(x):
+            if x is None:
+                return None
+            return C.c_void_p(x.data_ptr() if hasattr(x, "data_ptr") else int(x))
+        _check(lib().mp3g_plan_execute(self._h, p(d_gran), p(d_coef), p(d_state_in),
+                                       p(d_state_out), p(d_pcm),
+                                       C.c_void_p(stream) if stream else None))
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            lib().mp3g_plan_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,170 @@
+/*
+ * mp3g.h -- C-ABI of the MI355X-native MP3 Layer III granule-decode path.
+ *
+ * This library replaces the per-frame DSP seam of llehouerou/go-mp3:
+ *
+ *   func (f *Frame) Decode() []byte              reference internal/frame/frame.go:121-138
+ *
+ * i.e. requantize -> reorder -> MS/intensity stereo -> antialias -> hybrid
+ * IMDCT + overlap -> frequency inversion -> 32-subband polyphase synthesis ->
+ * s16le stereo PCM, for a BATCH of granules from many independent streams, on
+ * a gfx950 GPU.  The bitstream parse (frame header, side info, scale factors,
+ * Huffman, bit reservoir) stays on the host: the caller hands over exactly
+ * the fields `Decode` reads (reference frame.go:140-688)
+ * as packed granule descriptors plus int16 coefficients.
+ *
+ * Plain C types only: no torch, no HIP types in the signatures.  Every call
+ * returns an mp3g_status (0 = OK); nothing throws across the ABI and no caller
+ * pointer is retained after a call returns (cgo rule).
+ *
+ * Threading: a context / plan is single-threaded like mp3.Decoder
+ * (reference decode.go:27-33); distinct contexts may be used concurrently.
+ */
+#ifndef MP3G_H
+#define MP3G_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MP3G_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------ */
+typedef enum mp3g_status {
+  MP3G_OK = 0,
+  MP3G_ERR_INVALID_ARGUMENT = 1, /* null pointer, bad sizes, bad plan       */
+  MP3G_ERR_INVALID_GRANULE = 2,  /* descriptor field out of range (checked mode) */
+  MP3G_ERR_NO_DEVICE = 3,        /* no gfx950 device / HIP init failed      */
+  MP3G_ERR_DEVICE = 4,           /* HIP runtime error (see mp3g_last_error) */
+  MP3G_ERR_OUT_OF_MEMORY = 5,
+  MP3G_ERR_PARSE = 6,            /* host bitstream parse error (decoder API) */
+  MP3G_EOF = 7,                  /* end of stream (decoder API, io.EOF)      */
+  MP3G_ERR_UNSUPPORTED = 8       /* MPEG 2.5, layer I/II, free format, ...   */
+} mp3g_status;
+
+/* ---- boundary input: one granule descriptor ---------------------------- */
+/*
+ * Per-channel fields read by the DSP.  Field <- reference source:
+ *   count1           sideinfo.SideInfo.Count1, set by maindata/huffman.go:451
+ *   global_gain      sideinfo.go:115            scalefac_scale  sideinfo.go:151
+ *   preflag          sideinfo.go:149 (MPEG-1) / maindata.go:136 (MPEG-2)
+ *   win_switch_flag  sideinfo.go:117            block_type      sideinfo.go:119,143
+ *   mixed_block_flag sideinfo.go:120            subblock_gain   sideinfo.go:125
+ *   scalefac_l       maindata.MainData.ScalefacL[gr][ch] (maindata.go:34)
+ *   scalefac_s       maindata.MainData.ScalefacS[gr][ch] (maindata.go:35)
+ * 72 bytes, no padding.
+ */
+typedef struct mp3g_channel {
+  uint16_t count1;          /* 0..576: first line of the zero region          */
+  uint8_t global_gain;      /* 0..255                                         */
+  uint8_t scalefac_scale;   /* 0/1                                            */
+  uint8_t preflag;          /* 0/1                                            */
+  uint8_t win_switch_flag;  /* 0/1                                            */
+  uint8_t block_type;       /* 0..3                                           */
+  uint8_t mixed_block_flag; /* 0/1                                            */
+  uint8_t subblock_gain[3]; /* 0..7                                           */
+  uint8_t scalefac_l[22];   /* 0..15                                          */
+  uint8_t scalefac_s[13][3];/* [sfb][win], 0..15                              */
+} mp3g_channel;
+
+/*
+ * One granule = half an MPEG-1 frame (or a whole MPEG-2 LSF frame).
+ *   header : the raw 32-bit frameheader.FrameHeader (frameheader.go:29-137);
+ *            the DSP reads lsf, sampling-frequency index, mode, mode_ext from it.
+ *   gr     : granule index inside its frame (0/1), informational.
+ * 160 bytes (16-byte multiple so a descriptor is ten 16-B loads).
+ */
+typedef struct mp3g_granule {
+  uint32_t header;
+  uint32_t gr;
+  mp3g_channel ch[2];
+  uint8_t reserved[8];
+} mp3g_granule;
+
+/* Coefficients: int16 [n_granules][2][576], the integer Huffman output that
+ * the reference keeps as float32 in MainData.Is (maindata.go:36).  |x| <= 8206
+ * (15 + 13 linbits).  Mono granules leave [g][1][*] unread. */
+#define MP3G_LINES 576
+#define MP3G_COEF_PER_GRANULE (2 * MP3G_LINES)
+/* PCM: int16 [n_granules][576][2] = the bytes Decode() returns, concatenated
+ * (frame.go:134: granule gr at byte 2304*gr; mono duplicated, frame.go:671-678). */
+#define MP3G_PCM_BYTES_PER_GRANULE (MP3G_LINES * 2 * 2)
+
+/* ---- cross-granule DSP state (reference Frame.store / Frame.vVec) ------- */
+/* Layout identical to the reference fields (frame.go:48-49): copying a
+ * Frame's state in/out is a memcpy.  12,800 bytes. */
+typedef struct mp3g_state {
+  float store[2][32][18]; /* IMDCT overlap                          */
+  float vvec[2][1024];    /* polyphase FIFO, newest V block at [0:64] */
+} mp3g_state;
+
+/* ---- streams ------------------------------------------------------------ */
+/* A stream is a run of consecutive granules of one MP3 stream; the granules
+ * of stream s are [first_granule, first_granule + n_granules) in the granule
+ * and coefficient arrays, and its PCM goes to the same granule slots of the
+ * output.  State is carried inside the run exactly as frame.Read carries it
+ * (frame.go:110-113). */
+#define MP3G_STREAM_STATE_IN  1u /* start from state_in[s] (else zero state, = stream start / after Seek, decode.go:106-108) */
+#define MP3G_STREAM_STATE_OUT 2u /* write the state after the last granule to state_out[s] */
+typedef struct mp3g_stream {
+  uint64_t first_granule;
+  uint32_t n_granules;
+  uint32_t flags;
+} mp3g_stream;
+
+/* ---- decode modes -------------------------------------------------------- */
+#define MP3G_MODE_EXACT 0u   /* bit-exact vs the reference (linux/amd64 float semantics) */
+#define MP3G_MODE_FAST  1u   /* MFMA/fast-transform polyphase; |dPCM| <= 1 LSB          */
+#define MP3G_FLAG_CHECKED 0x100u /* validate descriptor ranges on the host first      */
+
+/* ---- library / device ---------------------------------------------------- */
+int mp3g_abi_version(void);
+/* Human-readable text for a status code; static storage. */
+const char* mp3g_status_string(int status);
+/* Last HIP/runtime error text of this thread (empty if none); static storage. */
+const char* mp3g_last_error(void);
+/* Number of visible gfx950 devices. */
+int mp3g_device_count(int* out_count);
+
+/* ---- checked-mode validation (host only, no GPU) ------------------------- */
+/* Returns MP3G_OK or MP3G_ERR_INVALID_GRANULE and the first bad index. */
+int mp3g_validate(const mp3g_granule* granules, const int16_t* coeffs,
+                  uint64_t n_granules, uint64_t* bad_index);
+
+/* ---- plans: device-resident work decomposition ---------------------------
+ * A plan splits every stream into chunks of `granules_per_chunk` granules
+ * (0 = automatic) processed by independent workgroups.  A chunk that does not
+ * start a stream re-derives its entry state from the two preceding granules
+ * (bit-identical to serial decode; DESIGN.md "halo").  The plan lives on
+ * `device` and can be executed many times (graph-capturable). */
+typedef struct mp3g_plan mp3g_plan;
+int mp3g_plan_create(int device, const mp3g_stream* streams, uint32_t n_streams,
+                     uint32_t granules_per_chunk, uint32_t mode, mp3g_plan** out_plan);
+int mp3g_plan_destroy(mp3g_plan* plan);
+/* Number of chunks (= workgroups launched) and granules incl. halo work. */
+int mp3g_plan_info(const mp3g_plan* plan, uint64_t* n_chunks, uint64_t* n_granules,
+                   uint64_t* n_halo_granules);
+
+/* Asynchronous execution on device-resident buffers.  All pointers are device
+ * pointers; `hip_stream` is a hipStream_t (NULL = default stream).  state_in /
+ * state_out may be NULL when no stream of the plan uses the flag. */
+int mp3g_plan_execute(mp3g_plan* plan, const mp3g_granule* d_granules,
+                      const int16_t* d_coeffs, const mp3g_state* d_state_in,
+                      mp3g_state* d_state_out, int16_t* d_pcm, void* hip_stream);
+
+/* ---- synchronous host-buffer decode (the cgo drop-in entry) --------------
+ * Copies the batch to `device`, decodes it and copies PCM (and state_out)
+ * back before returning.  Equivalent to calling Frame.Decode on every frame of
+ * every stream in order.  mode = MP3G_MODE_* | optional MP3G_FLAG_CHECKED. */
+int mp3g_decode_host(int device, const mp3g_granule* granules, const int16_t* coeffs,
+                     uint64_t n_granules, const mp3g_stream* streams, uint32_t n_streams,
+                     const mp3g_state* state_in, mp3g_state* state_out, int16_t* pcm,
+                     uint32_t mode);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MP3G_H */
