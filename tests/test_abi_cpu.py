@@ -1,0 +1,122 @@
+"""C-ABI checks that need no GPU: the library loads, exports exactly what
+include/mp3g.h declares, boundary struct layouts agree between C, the product
+binding and the oracle, host-side validation, and the exact-mode codegen
+contract (no FMA contraction in the device code)."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import mp3g
+import oracle
+from mp3g import synth
+
+from conftest import REPO
+
+HEADER = os.path.join(REPO, "include", "mp3g.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+\**(mp3g_\w+)\s*\(", src, re.M)))
+
+
+def test_exports_every_declared_symbol():
+    L = mp3g.lib()
+    names = declared_functions()
+    assert len(names) >= 10
+    for n in names:
+        assert hasattr(L, n), n
+    out = subprocess.check_output(["nm", "-D", "--defined-only", mp3g.lib_path()], text=True)
+    exported = set(re.findall(r" T (mp3g_\w+)", out))
+    assert set(names) == exported, set(names) ^ exported
+
+
+def test_struct_layouts_match_c(tmp_path):
+    prog = tmp_path / "layout.c"
+    fields = {
+        "mp3g_channel": ["count1", "global_gain", "scalefac_scale", "preflag", "win_switch_flag",
+                         "block_type", "mixed_block_flag", "subblock_gain", "scalefac_l", "scalefac_s"],
+        "mp3g_granule": ["header", "gr", "ch", "reserved"],
+        "mp3g_stream": ["first_granule", "n_granules", "flags"],
+        "mp3g_state": ["store", "vvec"],
+    }
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void){"]
+    for st, fs in fields.items():
+        lines.append(f'printf("{st} size %zu\\n", sizeof({st}));')
+        for f in fs:
+            lines.append(f'printf("{st} {f} %zu\\n", offsetof({st}, {f}));')
+    lines.append("return 0;}")
+    prog.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.check_call(["gcc", "-std=c11", str(prog), "-o", str(exe)])
+    c_layout = {}
+    for line in subprocess.check_output([str(exe)], text=True).splitlines():
+        st, f, v = line.split()
+        c_layout[(st, f)] = int(v)
+    dts = {"mp3g_channel": mp3g.CHANNEL_DTYPE, "mp3g_granule": mp3g.GRANULE_DTYPE,
+           "mp3g_stream": mp3g.STREAM_DTYPE, "mp3g_state": mp3g.STATE_DTYPE}
+    odts = {"mp3g_channel": oracle.CHANNEL_DTYPE, "mp3g_granule": oracle.GRANULE_DTYPE,
+            "mp3g_stream": oracle.STREAM_DTYPE, "mp3g_state": oracle.STATE_DTYPE}
+    for st, fs in fields.items():
+        assert c_layout[(st, "size")] == dts[st].itemsize == odts[st].itemsize
+        for f in fs:
+            assert c_layout[(st, f)] == dts[st].fields[f][1] == odts[st].fields[f][1], (st, f)
+
+
+def test_status_strings_and_version():
+    L = mp3g.lib()
+    assert L.mp3g_abi_version() == 1
+    for s in range(9):
+        assert L.mp3g_status_string(s) and L.mp3g_status_string(s) != b"unknown status"
+
+
+def test_validate_host_only():
+    g, c, s = synth.synth_batch(2, 20, seed=4, p_mixed=0.3)
+    assert mp3g.validate(g, c) == (0, 0)
+    cases = []
+    b = c.copy(); b[5, 1, 3] = 8207; cases.append((g, b, 5))          # |x| > 8206
+    gg = g.copy(); gg["ch"]["count1"][7, 0] = 577; cases.append((gg, c, 7))
+    gg = g.copy(); gg["header"][9] = 0xFFE39044; cases.append((gg, c, 9))  # MPEG 2.5
+    cc = c.copy(); n1 = int(g["ch"]["count1"][11, 0])
+    if n1 < 576:
+        cc[11, 0, n1] = 1; cases.append((g, cc, 11))  # nonzero above count1
+    gg = g.copy(); gg["ch"]["block_type"][13, 1] = 2; gg["ch"]["win_switch_flag"][13, 1] = 0
+    cases.append((gg, c, 13))
+    for gx, cx, k in cases:
+        st, bad = mp3g.validate(gx, cx)
+        assert st == 2 and bad == k
+    # MPEG-2 mixed blocks are rejected (the reference panics: maindata.go:139-178)
+    g2, c2, _ = synth.synth_batch(1, 20, seed=4, lsf=True)
+    assert mp3g.validate(g2, c2)[0] == 0
+    g2["ch"]["win_switch_flag"][3, 0] = 1
+    g2["ch"]["block_type"][3, 0] = 2
+    g2["ch"]["mixed_block_flag"][3, 0] = 1
+    assert mp3g.validate(g2, c2) == (2, 3)
+
+
+def test_no_cpu_fallback_without_gpu():
+    """On a machine without a gfx950 device the product fails loudly."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    assert mp3g.device_count() == 0
+    g, c, s = synth.synth_batch(1, 2, seed=1)
+    with pytest.raises(mp3g.Mp3gError) as e:
+        mp3g.decode_host(g, c, s)
+    assert e.value.status in (3, 4)
+
+
+def test_exact_kernel_has_no_fma():
+    """Exact mode contract: no fused multiply-add in the device code
+    (Go on linux/amd64 rounds every float32 product and sum)."""
+    csrc = os.path.join(REPO, "go-mp3_amd", "csrc")
+    subprocess.check_call(["make", "-s", "-C", csrc, "build/granule_exact.s"],
+                          stderr=subprocess.DEVNULL)
+    asm = open(os.path.join(csrc, "build", "granule_exact.s")).read()
+    body = asm.split(".end_amdhsa_kernel")[0]
+    assert "v_mul_f32" in body and "v_add_f32" in body
+    bad = re.findall(r"\b(v_fma\w*|v_fmac\w*|v_mac_\w*|v_mad_\w*f32|v_pk_fma\w*)\b", body)
+    assert not bad, sorted(set(bad))
