@@ -59,6 +59,17 @@ def build_workload(cfg, rank, seed_base=1):
                                     "streams_per_gpu": 1024, "frames_per_stream": 1024}
 
 
+def profiled_traffic(cfg):
+    """HBM bytes per launch from the newest rocprofv3 PMC summary in profiles/
+    (FETCH_SIZE x2 + WRITE_SIZE, KiB -> B; tools/summarize_profile.py), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_{cfg}.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    return d.get("hbm_bytes_per_launch_corrected"), os.path.relpath(files[-1], REPO)
+
+
 def main():
     args = parse()
     import torch
@@ -137,6 +148,7 @@ def main():
     out = None
     if rank == 0:
         achieved = frames_rank * BYTES_PER_FRAME / (kern_ms * 1e-3) / 1e9
+        traffic, traffic_src = profiled_traffic(args.config)
         out = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -156,7 +168,7 @@ def main():
                            halo_granules=pinfo["halo_granules"]),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
-                         "traffic": None,
+                         "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "granule_exact_kernel", "kernel_ms": round(kern_ms, 4),
                          "algorithmic_bytes_per_frame": BYTES_PER_FRAME},
         }

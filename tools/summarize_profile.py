@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Summarize rocprofv3 passes (tools/profile.sh) into profiles/<tag>_<cfg>.json + copy stats CSVs.
+
+HBM traffic per launch follows MI355X_MICROARCH.md (HBM section): FETCH_SIZE and
+WRITE_SIZE come from separate --pmc passes, are in KiB, and FETCH_SIZE reads
+exactly half the bytes of a wide coalesced stream on gfx950 -> doubled.
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+KERNEL = "granule"
+
+
+def counters(d):
+    f = glob.glob(os.path.join(d, "*counter_collection.csv"))
+    agg = collections.defaultdict(list)
+    if f:
+        for r in csv.DictReader(open(f[0])):
+            if KERNEL in r["Kernel_Name"]:
+                agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in agg.items()}
+
+
+def main(src, tag, cfg, dst="profiles", bytes_per_launch=None):
+    base = os.path.join(src, f"prof_{tag}_{cfg}")
+    stats = list(csv.DictReader(open(glob.glob(base + "_trace/*kernel_stats.csv")[0])))
+    k = [r for r in stats if KERNEL in r["Name"]][0]
+    fetch = counters(base + "_fetch").get("FETCH_SIZE")
+    write = counters(base + "_write").get("WRITE_SIZE")
+    sq = counters(base + "_sq")
+    avg_ns = float(k["AverageNs"])
+    out = {"tag": tag, "config": cfg, "kernel": k["Name"].split("(")[0], "calls": int(k["Calls"]),
+           "avg_ns": avg_ns, "min_ns": float(k["MinNs"]), "max_ns": float(k["MaxNs"])}
+    if fetch is not None and write is not None:
+        hbm = (2 * fetch + write) * 1024
+        out.update(fetch_kib=fetch, write_kib=write, hbm_bytes_per_launch_corrected=hbm,
+                   hbm_gbps=hbm / avg_ns)
+    if sq:
+        out["sq"] = sq
+        if "GRBM_GUI_ACTIVE" in sq:
+            out["clock_ghz_est"] = sq["GRBM_GUI_ACTIVE"] / 8 / avg_ns
+            # VALU issue slots: 256 CU x 4 SIMD, one wave64 VALU instruction per 2 cycles
+            slots = 256 * 4 * (sq["GRBM_GUI_ACTIVE"] / 8) / 2
+            if "SQ_INSTS_VALU" in sq:
+                out["valu_issue_util"] = sq["SQ_INSTS_VALU"] / slots
+    if bytes_per_launch:
+        out["algorithmic_bytes_per_launch"] = bytes_per_launch
+        out["algorithmic_gbps"] = bytes_per_launch / avg_ns
+    os.makedirs(dst, exist_ok=True)
+    json.dump(out, open(os.path.join(dst, f"{tag}_{cfg}.json"), "w"), indent=1)
+    for kind in ("trace",):
+        for f in glob.glob(base + f"_{kind}/*kernel_stats.csv"):
+            shutil.copyfile(f, os.path.join(dst, f"{tag}_{cfg}_kernel_stats.csv"))
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    src, tag, cfg = sys.argv[1:4]
+    bpl = int(sys.argv[4]) if len(sys.argv) > 4 else None
+    main(src, tag, cfg, bytes_per_launch=bpl)
