@@ -37,7 +37,18 @@ struct DspTables {
   // short-block info of line i in source (window-major) order:
   //   bits 0..3 short sfb, bits 4..5 window, bits 6..15 reordered destination
   uint16_t line_short[kCombos][576];
+  // inverse of the reorder permutation, indexed by DESTINATION line d:
+  //   bits 0..3 short sfb, bits 4..5 window of the source, bits 6..15 source line
+  uint16_t line_short_inv[kCombos][576];
   int8_t pretab[22];
+  // distinct rows of synthNWin (rows 0..16 and 32..48); the others follow
+  // bit-exactly: row 16+k = -row 16-k, row 48+k = row 48-k (k = 1..15)
+  float nwin_distinct[34][32];
+  // the 18 distinct columns of cosN36 (p = 0..8 and 18..26):
+  // col(17-p) = -col(p), col(53-p) = col(p)
+  float cos36_distinct[18][18];  // [m][q'], q' < 9 -> p = q', else p = 18 + (q' - 9)
+  // lines no antialias butterfly touches (80 of them), ascending
+  uint16_t aa_singles[80];
 };
 
 // Fills `t` (deterministic, thread-safe).

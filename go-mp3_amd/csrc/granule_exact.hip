@@ -18,18 +18,10 @@
 // state depends on (normally the two preceding ones; see plan_prologue) with
 // PCM output disabled -- the state is a pure function of those granules, so
 // the result is bit-identical to a serial decode.
-#include <hip/hip_runtime.h>
-
-#include "../../include/mp3g.h"
-#include "dsp_tables.h"
-#include "kernels.h"
-
-#pragma clang fp contract(off)
+// (compiled as part of kernels.hip)
 
 namespace mp3g {
-
-__device__ DspTables g_tab;
-
+namespace v1 {
 namespace {
 
 constexpr int kThreads = 256;
@@ -405,18 +397,5 @@ granule_exact_kernel(const ChunkDesc* __restrict__ chunks, const mp3g_granule* _
   if (cd.flags & kChunkStateOut) save_state(s, state_out + cd.stream, step);
 }
 
-hipError_t upload_tables(const DspTables& tables) {
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_tab), &tables, sizeof(DspTables), 0, hipMemcpyHostToDevice);
-}
-
-hipError_t launch_granule_exact(const ChunkDesc* d_chunks, uint32_t n_chunks,
-                                const mp3g_granule* d_gran, const int16_t* d_coef,
-                                const mp3g_state* d_state_in, mp3g_state* d_state_out,
-                                int16_t* d_pcm, hipStream_t stream) {
-  if (n_chunks == 0) return hipSuccess;
-  hipLaunchKernelGGL(granule_exact_kernel, dim3(n_chunks), dim3(kThreads), 0, stream, d_chunks,
-                     d_gran, d_coef, d_state_in, d_state_out, d_pcm);
-  return hipGetLastError();
-}
-
+}  // namespace v1
 }  // namespace mp3g

@@ -26,9 +26,13 @@ static_assert(sizeof(ChunkDesc) == 32, "ChunkDesc layout");
 
 // Host-side launchers (defined next to the kernels; no RDC needed).
 hipError_t upload_tables(const DspTables& tables);
-hipError_t launch_granule_exact(const ChunkDesc* d_chunks, uint32_t n_chunks,
-                                const mp3g_granule* d_gran, const int16_t* d_coef,
-                                const mp3g_state* d_state_in, mp3g_state* d_state_out,
-                                int16_t* d_pcm, hipStream_t stream);
+// Exact-mode kernel variants: v1 = per-phase reference implementation,
+// v2 = fused/register-blocked production kernel (default).
+constexpr int kVariantV1 = 1;
+constexpr int kVariantV2 = 2;
+hipError_t launch_granule(int variant, const ChunkDesc* d_chunks, uint32_t n_chunks,
+                          const mp3g_granule* d_gran, const int16_t* d_coef,
+                          const mp3g_state* d_state_in, mp3g_state* d_state_out, int16_t* d_pcm,
+                          hipStream_t stream);
 
 }  // namespace mp3g

@@ -1,0 +1,42 @@
+// kernels.hip -- the single device translation unit of libmp3g.so.
+//
+// Holds the constant tables (uploaded once per device) and both exact-mode
+// kernels: v1 (granule_exact.hip, the straightforward per-phase version, kept
+// as an on-device cross-check) and v2 (granule_fused.hip, the production
+// kernel).  One TU so both reach g_tab without relocatable device code.
+#include <hip/hip_runtime.h>
+
+#include "../../include/mp3g.h"
+#include "dsp_tables.h"
+#include "kernels.h"
+
+#pragma clang fp contract(off)
+
+namespace mp3g {
+__device__ DspTables g_tab;
+}  // namespace mp3g
+
+#include "granule_exact.hip"
+#include "granule_fused.hip"
+
+namespace mp3g {
+
+hipError_t upload_tables(const DspTables& tables) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_tab), &tables, sizeof(DspTables), 0, hipMemcpyHostToDevice);
+}
+
+hipError_t launch_granule(int variant, const ChunkDesc* d_chunks, uint32_t n_chunks,
+                          const mp3g_granule* d_gran, const int16_t* d_coef,
+                          const mp3g_state* d_state_in, mp3g_state* d_state_out, int16_t* d_pcm,
+                          hipStream_t stream) {
+  if (n_chunks == 0) return hipSuccess;
+  if (variant == kVariantV1)
+    hipLaunchKernelGGL(v1::granule_exact_kernel, dim3(n_chunks), dim3(256), 0, stream, d_chunks,
+                       d_gran, d_coef, d_state_in, d_state_out, d_pcm);
+  else
+    hipLaunchKernelGGL(v2::granule_fused_kernel, dim3(n_chunks), dim3(256), 0, stream, d_chunks,
+                       d_gran, d_coef, d_state_in, d_state_out, d_pcm);
+  return hipGetLastError();
+}
+
+}  // namespace mp3g

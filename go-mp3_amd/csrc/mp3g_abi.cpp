@@ -263,8 +263,9 @@ int mp3g_plan_execute(mp3g_plan* p, const mp3g_granule* d_gran, const int16_t* d
   for (const ChunkDesc& c : p->chunks) {
     if ((c.flags & kChunkStateOut) && !d_state_out) return fail(MP3G_ERR_INVALID_ARGUMENT, "state_out needed");
   }
-  HIP_TRY(launch_granule_exact(p->d_chunks, (uint32_t)p->chunks.size(), d_gran, d_coef, d_state_in,
-                               d_state_out, d_pcm, static_cast<hipStream_t>(hip_stream)));
+  const int variant = (p->mode & MP3G_FLAG_KERNEL_V1) ? kVariantV1 : kVariantV2;
+  HIP_TRY(launch_granule(variant, p->d_chunks, (uint32_t)p->chunks.size(), d_gran, d_coef, d_state_in,
+                         d_state_out, d_pcm, static_cast<hipStream_t>(hip_stream)));
   return MP3G_OK;
 }
 
@@ -287,7 +288,7 @@ int mp3g_decode_host(int device, const mp3g_granule* granules, const int16_t* co
     if (st) return st;
   }
   mp3g_plan* plan = nullptr;
-  int st = mp3g_plan_create(device, streams, n_streams, 0, mode & 0xffu, &plan);
+  int st = mp3g_plan_create(device, streams, n_streams, 0, mode & ~MP3G_FLAG_CHECKED, &plan);
   if (st) return st;
   DeviceGuard guard(device);
   void *dg = nullptr, *dc = nullptr, *dsi = nullptr, *dso = nullptr, *dp = nullptr;

@@ -119,6 +119,7 @@ typedef struct mp3g_stream {
 #define MP3G_MODE_EXACT 0u   /* bit-exact vs the reference (linux/amd64 float semantics) */
 #define MP3G_MODE_FAST  1u   /* MFMA/fast-transform polyphase; |dPCM| <= 1 LSB          */
 #define MP3G_FLAG_CHECKED 0x100u /* validate descriptor ranges on the host first      */
+#define MP3G_FLAG_KERNEL_V1 0x200u /* exact mode via the per-phase v1 kernel (cross-check) */
 
 /* ---- library / device ---------------------------------------------------- */
 int mp3g_abi_version(void);

@@ -113,10 +113,12 @@ def test_exact_kernel_has_no_fma():
     """Exact mode contract: no fused multiply-add in the device code
     (Go on linux/amd64 rounds every float32 product and sum)."""
     csrc = os.path.join(REPO, "go-mp3_amd", "csrc")
-    subprocess.check_call(["make", "-s", "-C", csrc, "build/granule_exact.s"],
+    subprocess.check_call(["make", "-s", "-C", csrc, "build/kernels.s"],
                           stderr=subprocess.DEVNULL)
-    asm = open(os.path.join(csrc, "build", "granule_exact.s")).read()
-    body = asm.split(".end_amdhsa_kernel")[0]
-    assert "v_mul_f32" in body and "v_add_f32" in body
-    bad = re.findall(r"\b(v_fma\w*|v_fmac\w*|v_mac_\w*|v_mad_\w*f32|v_pk_fma\w*)\b", body)
-    assert not bad, sorted(set(bad))
+    asm = open(os.path.join(csrc, "build", "kernels.s")).read()
+    kernels = re.findall(r"^(_ZN4mp3g2v\d\w+kernel\w*):(.*?)\.end_amdhsa_kernel", asm, re.S | re.M)
+    assert len(kernels) >= 2, [k[0] for k in kernels]
+    for name, body in kernels:
+        assert "v_mul_f32" in body and "v_add_f32" in body, name
+        bad = re.findall(r"\b(v_fma\w*|v_fmac\w*|v_mac_\w*|v_mad_\w*f32|v_pk_fma\w*)\b", body)
+        assert not bad, (name, sorted(set(bad)))

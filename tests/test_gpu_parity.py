@@ -21,7 +21,7 @@ def _dev(a):
     return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1)).cuda()
 
 
-def run_plan(mp3g, g, c, streams, chunk=0, state_in=None):
+def run_plan(mp3g, g, c, streams, chunk=0, state_in=None, mode=0):
     """Device-resident execution via mp3g_plan_* (torch owns the buffers)."""
     import torch
     n = len(g)
@@ -29,7 +29,7 @@ def run_plan(mp3g, g, c, streams, chunk=0, state_in=None):
     d_pcm = torch.zeros(n * 2304, dtype=torch.uint8, device="cuda")
     d_si = _dev(state_in) if state_in is not None else None
     d_so = torch.zeros(len(streams) * mp3g.STATE_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
-    plan = mp3g.Plan(streams, granules_per_chunk=chunk)
+    plan = mp3g.Plan(streams, granules_per_chunk=chunk, mode=mode)
     plan.execute(d_g, d_c, d_pcm, d_si, d_so, stream=torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     pcm = d_pcm.cpu().numpy().view(np.int16).reshape(n, 576, 2)
@@ -193,3 +193,16 @@ def test_c3_shape_bit_exact_and_batch_invariance(gpu):
     s_b["first_granule"] -= half
     p_b, _ = run_plan(gpu, g[half:], c[half:], s_b, chunk=7)
     assert_pcm_equal(np.concatenate([p_a, p_b]), want, "c3 split batches")
+
+
+@pytest.mark.parametrize("variant", ["v1", "v2"])
+def test_kernel_variants_agree(gpu, captured, variant):
+    """Both exact kernels (per-phase v1, fused v2) are bit-exact on every case."""
+    mode = gpu.FLAG_KERNEL_V1 if variant == "v1" else 0
+    g, c, want = captured["classic_lame.mp3"]
+    pcm, _ = run_plan(gpu, g, c, gpu.streams_for([len(g)]), chunk=7, mode=mode)
+    assert_pcm_equal(pcm, want, variant)
+    g, c, s = synth.synth_batch(4, 40, seed=77, p_mixed=0.4, p_is=0.5, p_event=0.1)
+    want, _ = oracle.dsp_streams(g, c, s)
+    pcm, _ = run_plan(gpu, g, c, s, chunk=3, mode=mode)
+    assert_pcm_equal(pcm, want, variant + " synth")
