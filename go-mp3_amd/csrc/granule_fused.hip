@@ -33,6 +33,8 @@ constexpr int kThreads = 256;
 // granule's 18 blocks; after a granule slots 18..33 move to 0..15.  Static
 // slots give immediate-offset LDS addressing in the window sum.
 constexpr int kRing = 34;
+constexpr int kNStride = 36;
+constexpr int kSStride = 36;  // 16 different time slots read by one b128 group -> distinct bank quads
 
 struct PcmRaw {
   int16_t pcm[576 * 2];   // staged s16 stereo output of the last decoded granule
@@ -45,12 +47,12 @@ struct __align__(16) Smem {
     int flags[256];       // prologue scratch
   } a;
   union {
-    float xt[2][18][32];  // hybrid output, transposed: [ch][time slot][subband]
+    float xt[2][18][kSStride];  // hybrid output, transposed: [ch][time slot][subband] (padded rows)
     PcmRaw io;            // (dead while xt is live)
   } b;
   float store[2][576];    // IMDCT overlap == Frame.store[ch][sb][i]
   float ring[2][kRing][64];
-  float nrow[34][32];
+  float nrow[34][kNStride];  // row stride 36: the 16 rows a ds_read_b128 group reads hit 16 distinct bank quads
   float c36[18][18];
   float win[4][36];
   float cos12[6][12];
@@ -290,8 +292,8 @@ __device__ void phase_matrix(Smem& s, const VLane& L, int nch) {
     const float4 n5 = *reinterpret_cast<const float4*>(N5 + j);
     float4 sv[5];
 #pragma unroll
-    for (int k = 0; k < 4; k++) sv[k] = *reinterpret_cast<const float4*>(S + (q4 + 4 * k) * 32 + j);
-    sv[4] = *reinterpret_cast<const float4*>(S + L.ss5 * 32 + j);
+    for (int k = 0; k < 4; k++) sv[k] = *reinterpret_cast<const float4*>(S + (q4 + 4 * k) * kSStride + j);
+    sv[4] = *reinterpret_cast<const float4*>(S + L.ss5 * kSStride + j);
 #pragma unroll
     for (int k = 0; k < 4; k++) acc[k] = acc[k] + nv.x * sv[k].x;
     acc[4] = acc[4] + n5.x * sv[4].x;
@@ -443,7 +445,7 @@ granule_fused_kernel(const ChunkDesc* __restrict__ chunks, const mp3g_granule* _
   const ChunkDesc cd = chunks[blockIdx.x];
   const int t = threadIdx.x;
 
-  for (int k = t; k < 34 * 32; k += kThreads) (&s.nrow[0][0])[k] = (&g_tab.nwin_distinct[0][0])[k];
+  for (int k = t; k < 34 * 32; k += kThreads) s.nrow[k >> 5][k & 31] = (&g_tab.nwin_distinct[0][0])[k];
   for (int k = t; k < 18 * 18; k += kThreads) (&s.c36[0][0])[k] = (&g_tab.cos36_distinct[0][0])[k];
   for (int k = t; k < 4 * 36; k += kThreads) (&s.win[0][0])[k] = (&g_tab.imdct_win[0][0])[k];
   for (int k = t; k < 6 * 12; k += kThreads) (&s.cos12[0][0])[k] = (&g_tab.cos12[0][0])[k];
