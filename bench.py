@@ -30,6 +30,10 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 METRIC = "MP3 frames/sec (44.1 kHz stereo 128 kbps) at 1/2/4/8 GPUs; max |ΔPCM| LSB"
 
 
+MODES = {"exact": ("exact (bit-exact vs reference)", "mp3g::v2::granule_fused_kernel"),
+         "fast": ("fast (+-1 LSB vs reference)", "mp3g::v3::granule_fast_kernel")}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -37,6 +41,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", choices=["c2", "c3"], default="c2")
     ap.add_argument("--chunk", type=int, default=0, help="granules per chunk (0 = auto)")
+    ap.add_argument("--mode", choices=["exact", "fast"], default="exact",
+                    help="exact: bit-exact kernel (v2); fast: +-1 LSB kernel (v3)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-repeats", type=int, default=5)
     ap.add_argument("--gather", action="store_true", help="also time an RCCL PCM gather to rank 0")
@@ -59,15 +65,17 @@ def build_workload(cfg, rank, seed_base=1):
                                     "streams_per_gpu": 1024, "frames_per_stream": 1024}
 
 
-def profiled_traffic(cfg):
+def profiled_traffic(cfg, kernel):
     """HBM bytes per launch from the newest rocprofv3 PMC summary in profiles/
-    (FETCH_SIZE x2 + WRITE_SIZE, KiB -> B; tools/summarize_profile.py), or None."""
+    for this config and kernel (FETCH_SIZE x2 + WRITE_SIZE, KiB -> B;
+    tools/summarize_profile.py), or None."""
     import glob
     files = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_{cfg}.json")))
-    if not files:
-        return None, None
-    d = json.load(open(files[-1]))
-    return d.get("hbm_bytes_per_launch_corrected"), os.path.relpath(files[-1], REPO)
+    for f in reversed(files):
+        d = json.load(open(f))
+        if d.get("kernel") == kernel and d.get("hbm_bytes_per_launch_corrected"):
+            return d["hbm_bytes_per_launch_corrected"], os.path.relpath(f, REPO)
+    return None, None
 
 
 def main():
@@ -99,7 +107,8 @@ def main():
         d_c = torch.from_numpy(c.reshape(-1).copy()).to(dev)
         n_gran = len(g)
     d_pcm = torch.empty(n_gran * 1152, dtype=torch.int16, device=dev)
-    plan = mp3g.Plan(streams, granules_per_chunk=args.chunk, device=local)
+    mode = mp3g.MODE_FAST if args.mode == "fast" else mp3g.MODE_EXACT
+    plan = mp3g.Plan(streams, granules_per_chunk=args.chunk, mode=mode, device=local)
     pinfo = plan.info()
     stream = torch.cuda.current_stream(dev)
     h = stream.cuda_stream
@@ -148,7 +157,7 @@ def main():
     out = None
     if rank == 0:
         achieved = frames_rank * BYTES_PER_FRAME / (kern_ms * 1e-3) / 1e9
-        traffic, traffic_src = profiled_traffic(args.config)
+        traffic, traffic_src = profiled_traffic(args.config, MODES[args.mode][1])
         out = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -162,14 +171,14 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
-            "config": dict(cfg_info, mode="exact (bit-exact vs reference)",
+            "config": dict(cfg_info, mode=MODES[args.mode][0],
                            parallelism=f"{world} independent ranks (stream sharding)",
                            granules_per_gpu=int(n_gran), chunks=pinfo["chunks"],
                            halo_granules=pinfo["halo_granules"]),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
                          "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "granule_exact_kernel", "kernel_ms": round(kern_ms, 4),
+                         "kernel": MODES[args.mode][1], "kernel_ms": round(kern_ms, 4),
                          "algorithmic_bytes_per_frame": BYTES_PER_FRAME},
         }
         if gather_ms is not None:

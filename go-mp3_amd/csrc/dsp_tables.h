@@ -54,4 +54,25 @@ struct DspTables {
 // Fills `t` (deterministic, thread-safe).
 void build_tables(DspTables* t);
 
+// Tables of the fast mode (MP3G_MODE_FAST, granule_fast.hip), derived from the
+// exact tables above with exact sign/index identities only, so every constant
+// is the reference's own float32 value.
+//   V = synthNWin * S (64 x 32) is computed from its 32 distinct values
+//   X[m] = sum_k cos((2k+1) m pi / 64) s[k], folded even/odd:
+//   X[m] = sum_{k<16} dct[m][k] * (m even ? s[k] + s[31-k] : s[k] - s[31-k]),
+//   dct[m][k] = nwin[m-16][k] (m >= 16), -nwin[48-m][k] (m < 16).
+//   V[i] = X[16+i] (i < 16), 0 (i = 16), -X[48-i] (16 < i < 48), -X[i-48] (i >= 48).
+//   The window sum pcm[i] = sum_j D[32j+i] * (j even ? V_j[i] : V_j[32+i])
+//   reads X_j[a_i] (j even) and X_j[b_i] (j odd) with the signs folded into
+//   dwin[i][j] (a_i = 16+i | 48-i, b_i = 16-i | i-16).
+struct FastTables {
+  float c36[18][18];   // distinct cosN36 columns (= DspTables::cos36_distinct)
+  float cos12[6][12];
+  float win[4][36];
+  float dct[32][16];
+  float dwin[32][16];
+  float aa_cs[8], aa_ca[8];
+};
+void build_fast_tables(const DspTables& t, FastTables* f);
+
 }  // namespace mp3g

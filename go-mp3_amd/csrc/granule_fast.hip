@@ -1,0 +1,380 @@
+// granule_fast.hip -- MP3G_MODE_FAST granule decode, v3 (gfx950).
+//
+// Same contract, chunk/halo decomposition and front end as the exact kernels
+// (reference internal/frame/frame.go:121-688), but the three transforms are
+// evaluated in reassociated, FMA-contracted float32, so PCM is within +-1 LSB
+// of the reference instead of bit-identical (north star tolerance; measured
+// by tests/test_gpu_parity.py::test_fast_mode_*).
+//
+// Work decomposition: ONE WAVE PER CHUNK.  A 64-lane workgroup walks its chunk
+// granule by granule with no s_barrier-level cross-wave traffic:
+//   front end   lane = (ch, sb): the 18 lines of its subband -- requantize
+//               (gather through the reorder table), MS/IS with the partner
+//               channel via a lane^32 shuffle, antialias butterflies with the
+//               neighbouring subbands via lane+-1 shuffles;
+//   IMDCT       lane = (ch, sb): 36-point (or 3 x 12-point) IMDCT in registers,
+//               the overlap `store` lives in the lane's VGPRs for the whole
+//               chunk, frequency inversion;
+//   matrixing   V = synthNWin * S has 32 distinct values X (DSP identity,
+//               dsp_tables.h FastTables); the lane pair (sb, 31-sb) folds
+//               S into even/odd halves (lane^31 shuffle), then lane = (ch, m)
+//               computes X_m for all 18 time slots: 16 FMAs per value against
+//               its coefficient row held in VGPRs;
+//   window      lane = (ch, i): 16-tap window over the X ring with the V->X
+//               signs folded into the taps (VGPRs), 18 outputs per lane, s16
+//               packed (L,R) with one lane^32 exchange per slot pair.
+// LDS per wave ~14 KB (raw/eo union, X ring 2 x 34 x 32, descriptor, IMDCT
+// windows) -> 11 resident waves per CU.
+// (compiled as part of kernels.hip, after granule_common.hip)
+#pragma clang fp contract(fast)
+
+namespace mp3g {
+namespace v3 {
+namespace {
+
+using common::hdr_combo;
+using common::hdr_mode;
+using common::hdr_nch;
+using common::pcm_sample;
+
+constexpr int kLanes = 64;
+constexpr int kRing = 34;  // X slots: 0..15 history (slot 15 newest), 16..33 current granule
+
+struct __align__(16) WaveSmem {
+  union {
+    int16_t raw[2][576];   // Huffman integers of the current granule
+    float eo[2][18][32];   // folded matrixing input [ch][slot][k]: even part k<16, odd part 16+k
+  } a;
+  float ring[2][kRing][32];
+  float win[4][36];        // imdctWinData
+  float c36t[18][20];      // distinct cosN36 columns, transposed [q][m] (rows padded to 5 x float4)
+  float c12t[12][8];       // cosN12 transposed [p][m] (rows padded to 2 x float4)
+  mp3g_granule desc;
+};
+
+__device__ __forceinline__ void load_granule(WaveSmem& s, const mp3g_granule* gran, const int16_t* coef,
+                                             uint64_t g) {
+  const int t = threadIdx.x;
+  const uint4* src = reinterpret_cast<const uint4*>(coef + g * MP3G_COEF_PER_GRANULE);
+  uint4* dst = reinterpret_cast<uint4*>(&s.a.raw[0][0]);
+  dst[t] = src[t];
+  dst[t + 64] = src[t + 64];
+  if (t < 16) dst[t + 128] = src[t + 128];
+  if (t < 10) reinterpret_cast<uint4*>(&s.desc)[t] = reinterpret_cast<const uint4*>(gran + g)[t];
+}
+
+// Replay start of a chunk (same decision as v2::plan_prologue, with wave
+// ballots instead of a workgroup scan).
+__device__ void prologue(const ChunkDesc& cd, const mp3g_granule* gran, uint64_t* w_out, int init_in[2]) {
+  const uint64_t c0 = cd.out_first, s0 = cd.stream_first;
+  const bool have_in = cd.flags & kChunkStateIn;
+  if (c0 == s0) {
+    *w_out = c0;
+    init_in[0] = init_in[1] = have_in;
+    return;
+  }
+  const uint64_t start0 = (c0 >= 2 && c0 - 2 > s0) ? c0 - 2 : s0;
+  const bool st1 = hdr_nch(gran[c0 - 1].header) == 2;
+  const bool st2 = (c0 >= 2 && c0 - 2 >= s0) ? hdr_nch(gran[c0 - 2].header) == 2 : false;
+  if (st1 && st2) {
+    *w_out = start0;
+    init_in[0] = init_in[1] = (start0 == s0) && have_in;
+    return;
+  }
+  int any = 0;
+  for (uint32_t k = threadIdx.x; k < cd.n_out; k += kLanes) any |= hdr_nch(gran[c0 + k].header) == 2;
+  const bool need1 = __ballot(any) != 0 || (cd.flags & kChunkStateOut);
+  uint64_t start1 = c0;
+  bool ch1_from_in = false;
+  if (need1) {
+    int found = 0;
+    uint64_t p2 = 0;
+    for (uint64_t hi = c0; hi > s0 && found < 2;) {
+      const uint64_t lo = hi - s0 > kLanes ? hi - kLanes : s0;
+      const uint64_t g = hi - 1 - threadIdx.x;
+      const bool stereo = (threadIdx.x < hi - lo) && hdr_nch(gran[g].header) == 2;
+      uint64_t m = __ballot(stereo);
+      while (m && found < 2) {
+        const int b = __ffsll((unsigned long long)m) - 1;
+        found++;
+        if (found == 2) p2 = hi - 1 - b;
+        m &= m - 1;
+      }
+      hi = lo;
+    }
+    if (found == 2) start1 = p2;
+    else if (found == 1) start1 = s0;
+    else ch1_from_in = true;
+  }
+  const uint64_t w = start0 < start1 ? start0 : start1;
+  *w_out = w;
+  init_in[0] = (w == s0) && have_in;
+  init_in[1] = ch1_from_in ? have_in : ((w == s0) && have_in);
+}
+
+// X of a V block: X[m] = V[m-16] (m >= 16), -V[48-m] (m < 16).
+__device__ __forceinline__ float x_from_v(const float* v, int m) { return m >= 16 ? v[m - 16] : -v[48 - m]; }
+// V of an X vector (inverse identity; V[16] = 0).
+__device__ __forceinline__ float v_from_x(const float* x, int i) {
+  if (i < 16) return x[16 + i];
+  if (i == 16) return 0.0f;
+  if (i < 48) return -x[48 - i];
+  return -x[i - 48];
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(kLanes, 2)
+granule_fast_kernel(const ChunkDesc* __restrict__ chunks, const mp3g_granule* __restrict__ gran,
+                    const int16_t* __restrict__ coef, const mp3g_state* __restrict__ state_in,
+                    mp3g_state* __restrict__ state_out, int16_t* __restrict__ pcm) {
+  __shared__ WaveSmem s;
+  const ChunkDesc cd = chunks[blockIdx.x];
+  const int lane = threadIdx.x;
+  const int ch = lane >> 5, k = lane & 31;
+
+  // per-lane constants: matrixing row X_k and window taps of output index k
+  float dct[16], dw[16];
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    dct[j] = g_fast.dct[k][j];
+    dw[j] = g_fast.dwin[k][j];
+  }
+  const int ia = k < 16 ? 16 + k : (k == 16 ? 0 : 48 - k);
+  const int ib = k < 16 ? 16 - k : k - 16;
+  for (int e = lane; e < 4 * 36; e += kLanes) (&s.win[0][0])[e] = (&g_fast.win[0][0])[e];
+  for (int e = lane; e < 18 * 20; e += kLanes) {
+    const int q = e / 20, m = e % 20;
+    s.c36t[q][m] = m < 18 ? g_fast.c36[m][q] : 0.0f;
+  }
+  for (int e = lane; e < 12 * 8; e += kLanes) {
+    const int p = e >> 3, m = e & 7;
+    s.c12t[p][m] = m < 6 ? g_fast.cos12[m][p] : 0.0f;
+  }
+
+  uint64_t w;
+  int init_in[2];
+  prologue(cd, gran, &w, init_in);
+  const mp3g_state* sin = state_in ? state_in + cd.stream : nullptr;
+
+  // entry state: overlap store in registers, V history as X vectors
+  float st[18];
+  {
+    const bool from_in = init_in[ch] && sin;
+#pragma unroll
+    for (int j = 0; j < 18; j++) st[j] = from_in ? sin->store[ch][k][j] : 0.0f;
+    for (int e = lane; e < 2 * 16 * 32; e += kLanes) {
+      const int c = e >> 9, blk = (e >> 5) & 15, m = e & 31;
+      const bool in = init_in[c] && sin;
+      s.ring[c][15 - blk][m] = in ? x_from_v(&sin->vvec[c][64 * blk], m) : 0.0f;
+    }
+  }
+
+  const uint64_t end = cd.out_first + cd.n_out;
+  if (w < end) load_granule(s, gran, coef, w);
+  __syncthreads();
+
+  for (uint64_t g = w; g < end; g++) {
+    const bool out = g >= cd.out_first;
+    const uint32_t h = s.desc.header;
+    const int nch = hdr_nch(h), combo = hdr_combo(h);
+    const bool act = ch < nch;
+    // lanes of an absent channel mirror channel 0's block layout (no extra divergence)
+    const mp3g_channel& C = s.desc.ch[act ? ch : 0];
+
+    // prefetch the next granule (lands during this one)
+    const bool more = g + 1 < end;
+    uint4 p0 = {0, 0, 0, 0}, p1 = p0, p2 = p0, pd = p0;
+    if (more) {
+      const uint4* src = reinterpret_cast<const uint4*>(coef + (g + 1) * MP3G_COEF_PER_GRANULE);
+      p0 = src[lane];
+      p1 = src[lane + 64];
+      if (lane < 16) p2 = src[lane + 128];
+      if (lane < 10) pd = reinterpret_cast<const uint4*>(gran + g + 1)[lane];
+    }
+
+    // ---- front end: requantize + stereo + antialias, lane = (ch, sb = k) ----
+    float x[18];
+#pragma unroll
+    for (int j = 0; j < 18; j++) x[j] = act ? common::requant_line(s.a.raw[ch], C, 18 * k + j, combo) : 0.0f;
+    if (nch == 2 && hdr_mode(h) == 1 && (h & 0x30u)) {
+#pragma unroll
+      for (int j = 0; j < 18; j++) {
+        const float o = __shfl_xor(x[j], 32);
+        float l = ch ? o : x[j], r = ch ? x[j] : o;
+        common::stereo_line(s.desc, h, combo, 18 * k + j, l, r);
+        x[j] = ch ? r : l;
+      }
+    }
+    {
+      const bool sw = C.win_switch_flag == 1 && C.block_type == 2;
+      const bool skip = !act || (sw && C.mixed_block_flag == 0);
+      const int sblim = (sw && C.mixed_block_flag == 1) ? 2 : 32;
+      const bool lower = !skip && k >= 1 && k < sblim;     // butterfly with subband k-1
+      const bool upper = !skip && k < 31 && k + 1 < sblim;  // butterfly with subband k+1
+      float up[8], dn[8];
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        up[i] = __shfl_up(x[17 - i], 1);  // x_{k-1}[17-i]
+        dn[i] = __shfl_down(x[i], 1);     // x_{k+1}[i]
+      }
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        const float cs = g_fast.aa_cs[i], ca = g_fast.aa_ca[i];
+        const float ui = x[i], li = x[17 - i];
+        if (lower) x[i] = ui * cs + up[i] * ca;
+        if (upper) x[17 - i] = li * cs - dn[i] * ca;
+      }
+    }
+
+    // ---- IMDCT + overlap + frequency inversion ----
+    float o[18];
+    {
+      int bt = C.block_type & 3;
+      if (C.win_switch_flag == 1 && C.mixed_block_flag == 1 && k < 2) bt = 0;
+      float r[36];
+      if (bt == 2) {
+#pragma unroll
+        for (int p = 0; p < 36; p++) r[p] = 0.0f;
+#pragma unroll
+        for (int p = 0; p < 12; p++) {
+          const float4 c0 = *reinterpret_cast<const float4*>(&s.c12t[p][0]);
+          const float2 c1 = *reinterpret_cast<const float2*>(&s.c12t[p][4]);
+          const float cp[6] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y};
+          const float wp = s.win[2][p];
+#pragma unroll
+          for (int wi = 0; wi < 3; wi++) {
+            float sum = 0.0f;
+#pragma unroll
+            for (int m = 0; m < 6; m++) sum += x[wi + 3 * m] * cp[m];
+            r[6 * wi + p + 6] += sum * wp;
+          }
+        }
+      } else {
+        const float* W = s.win[bt];
+#pragma unroll
+        for (int q = 0; q < 9; q++) {
+          float za = 0.0f, zb = 0.0f;
+          const float4* ca = reinterpret_cast<const float4*>(&s.c36t[q][0]);
+          const float4* cb = reinterpret_cast<const float4*>(&s.c36t[9 + q][0]);
+#pragma unroll
+          for (int m4 = 0; m4 < 5; m4++) {
+            const float4 a = ca[m4], b = cb[m4];
+            const float av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+              if (4 * m4 + e < 18) {
+                za += x[4 * m4 + e] * av[e];
+                zb += x[4 * m4 + e] * bv[e];
+              }
+            }
+          }
+          r[q] = za * W[q];
+          r[17 - q] = -za * W[17 - q];
+          r[18 + q] = zb * W[18 + q];
+          r[35 - q] = zb * W[35 - q];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 18; j++) {
+        o[j] = r[j] + st[j];
+        if (act) st[j] = r[18 + j];
+        if ((k & 1) && (j & 1)) o[j] = -o[j];
+      }
+    }
+    __syncthreads();  // raw[] fully consumed before eo[] (same LDS) is written
+
+    // ---- even/odd fold of S across the subband pair (k, 31-k) ----
+#pragma unroll
+    for (int j = 0; j < 18; j++) {
+      const float oth = __shfl_xor(o[j], 31);
+      if (act) s.a.eo[ch][j][k < 16 ? k : 47 - k] = k < 16 ? o[j] + oth : oth - o[j];
+    }
+    __syncthreads();
+
+    // ---- matrixing: X_k for the 18 slots of this granule ----
+    bool need_v = true;
+    if (!out && g + 1 < cd.out_first) need_v = hdr_nch(gran[g + 1].header) < nch;
+    if (need_v && act) {
+      const float* E = &s.a.eo[ch][0][(k & 1) * 16];
+#pragma unroll 2
+      for (int ss = 0; ss < 18; ss++) {
+        const float4* e4 = reinterpret_cast<const float4*>(E + 32 * ss);
+        float acc = 0.0f;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const float4 e = e4[q];
+          acc += dct[4 * q] * e.x;
+          acc += dct[4 * q + 1] * e.y;
+          acc += dct[4 * q + 2] * e.z;
+          acc += dct[4 * q + 3] * e.w;
+        }
+        s.ring[ch][16 + ss][k] = acc;
+      }
+    }
+    __syncthreads();
+
+    // ---- 16-tap window over the X ring -> s16 PCM ----
+    if (out && act) {
+      float acc[18];
+#pragma unroll
+      for (int ss = 0; ss < 18; ss++) acc[ss] = 0.0f;
+      const float* R = &s.ring[ch][0][0];
+#pragma unroll
+      for (int u = -15; u < 18; u++) {
+        const float xa = R[(16 + u) * 32 + ia];
+        const float xb = R[(16 + u) * 32 + ib];
+#pragma unroll
+        for (int ss = (u > 0 ? u : 0); ss < 18 && ss <= u + 15; ss++) {
+          const int j = ss - u;
+          acc[ss] += dw[j] * ((j & 1) ? xb : xa);
+        }
+      }
+      uint32_t* dst = reinterpret_cast<uint32_t*>(pcm + g * 1152);
+      if (nch == 2) {
+#pragma unroll
+        for (int q = 0; q < 9; q++) {
+          const int a = pcm_sample(acc[2 * q]), b = pcm_sample(acc[2 * q + 1]);
+          const int got = __shfl_xor(ch ? a : b, 32);
+          // lane (0,k) stores slot 2q, lane (1,k) slot 2q+1: (L, R) = low, high half
+          const int L = ch ? got : a, Rr = ch ? b : got;
+          dst[32 * (2 * q + ch) + k] = (uint32_t)(L & 0xffff) | ((uint32_t)Rr << 16);
+        }
+      } else {
+#pragma unroll
+        for (int ss = 0; ss < 18; ss++) {
+          const uint32_t v = (uint32_t)pcm_sample(acc[ss]) & 0xffffu;
+          dst[32 * ss + k] = v | (v << 16);
+        }
+      }
+    }
+    __syncthreads();  // ring reads done
+
+    // ---- history shift (channels this granule touched) + next granule in ----
+    for (int e = lane; e < nch * 128; e += kLanes) {
+      const int c = e >> 7, r4 = e & 127;
+      reinterpret_cast<float4*>(&s.ring[c][0][0])[r4] = reinterpret_cast<const float4*>(&s.ring[c][18][0])[r4];
+    }
+    if (more) {
+      uint4* dst = reinterpret_cast<uint4*>(&s.a.raw[0][0]);
+      dst[lane] = p0;
+      dst[lane + 64] = p1;
+      if (lane < 16) dst[lane + 128] = p2;
+      if (lane < 10) reinterpret_cast<uint4*>(&s.desc)[lane] = pd;
+    }
+    __syncthreads();
+  }
+
+  if (cd.flags & kChunkStateOut) {
+    mp3g_state* so = state_out + cd.stream;
+#pragma unroll
+    for (int j = 0; j < 18; j++) so->store[ch][k][j] = st[j];
+    for (int e = lane; e < 2 * 1024; e += kLanes) {
+      const int c = e >> 10, blk = (e >> 6) & 15, i = e & 63;
+      so->vvec[c][64 * blk + i] = v_from_x(s.ring[c][15 - blk], i);
+    }
+  }
+}
+
+}  // namespace v3
+}  // namespace mp3g

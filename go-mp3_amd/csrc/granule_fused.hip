@@ -60,100 +60,18 @@ struct __align__(16) Smem {
   mp3g_granule desc;
 };
 
-__device__ __forceinline__ int hdr_mode(uint32_t h) { return (int)((h >> 6) & 3u); }
-__device__ __forceinline__ int hdr_nch(uint32_t h) { return hdr_mode(h) == 3 ? 1 : 2; }
-__device__ __forceinline__ int hdr_combo(uint32_t h) {
-  const int lsf = ((h >> 19) & 3u) == 3u ? 0 : 1;
-  int sf = (int)((h >> 10) & 3u);
-  sf = sf > 2 ? 2 : sf;
-  return lsf * 3 + sf;
-}
+using common::hdr_combo;
+using common::hdr_mode;
+using common::hdr_nch;
+using common::pcm_sample;
 
-__device__ __forceinline__ int pcm_sample(float sum) {
-  const float t = sum * 32767.0f;
-  if (!(t == t) || fabsf(t) >= 9.2233720368547758e18f) return -32767;
-  return (int)fminf(fmaxf(t, -32767.0f), 32767.0f);
-}
-
-// ---- front end: requantize (gather) for one output line of one channel ----
 __device__ __forceinline__ float requant_line(const Smem& s, const mp3g_channel& C, int ch, int L,
                                               int combo) {
-  const bool shortblk = C.win_switch_flag == 1 && C.block_type == 2;
-  const bool mixed = C.mixed_block_flag != 0;
-  const int count1 = C.count1;
-  int src = L, sfb, win = 0;
-  bool process, is_long;
-  if (!shortblk) {
-    process = L < count1;
-    is_long = true;
-    sfb = g_tab.line_long_sfb[combo][L];
-  } else if (mixed && L < 36) {
-    process = true;
-    is_long = true;
-    sfb = g_tab.line_long_sfb[combo][L];
-  } else {
-    const int inv = g_tab.line_short_inv[combo][L];
-    sfb = inv & 15;
-    const int bstart = 3 * (int)g_tab.sfb_short[combo][sfb];
-    process = bstart < count1;
-    const bool reordered = sfb == (mixed ? 3 : 0) || bstart < count1;
-    if (reordered) {
-      src = inv >> 6;
-      win = (inv >> 4) & 3;
-    } else {
-      win = (g_tab.line_short[combo][L] >> 4) & 3;  // not moved: window of L itself
-    }
-    is_long = false;
-  }
-  const int x = s.b.io.raw[ch][src];
-  if (!process) return (float)x;
-  const int sfmul = C.scalefac_scale != 0 ? 4 : 2;
-  int n4;
-  if (is_long)
-    n4 = (int)C.global_gain - 210 -
-         sfmul * ((int)C.scalefac_l[sfb] + (int)C.preflag * (int)g_tab.pretab[sfb]);
-  else
-    n4 = (int)C.global_gain - 210 - 8 * (int)C.subblock_gain[win] - sfmul * (int)C.scalefac_s[sfb][win];
-  float v = ldexpf(g_tab.req[n4 & 3][min(abs(x), 8206)], n4 >> 2);
-  return x < 0 ? -v : v;
+  return common::requant_line(s.b.io.raw[ch], C, L, combo);
 }
-
-// MS / IS of line L (frame.go:361-420), both channels in registers.
 __device__ __forceinline__ void stereo_line(const Smem& s, uint32_t h, int combo, int L, float& l,
                                             float& r) {
-  if (hdr_mode(h) != 1) return;
-  const mp3g_channel& C0 = s.desc.ch[0];
-  const int c1r = s.desc.ch[1].count1;
-  if ((h & 0x20u) && L < max((int)C0.count1, c1r)) {
-    const float inv_sqrt2 = 0.70710678118654752440f;
-    const float nl = (l + r) * inv_sqrt2;
-    const float nr = (l - r) * inv_sqrt2;
-    l = nl;
-    r = nr;
-  }
-  if (h & 0x10u) {
-    const bool short0 = C0.win_switch_flag == 1 && C0.block_type == 2;
-    const bool mixed0 = C0.mixed_block_flag != 0;
-    const int sfl = g_tab.line_long_sfb[combo][L];
-    const int info = g_tab.line_short[combo][L];
-    const int sfs = info & 15, win = (info >> 4) & 3;
-    const bool long_pass = !short0 ? (sfl < 21) : (mixed0 && sfl < 8);
-    if (long_pass && (int)g_tab.sfb_long[combo][sfl] >= c1r) {
-      const int pos = C0.scalefac_l[sfl];
-      if (pos < 7) {
-        l = l * g_tab.is_ratio[pos][0];
-        r = r * g_tab.is_ratio[pos][1];
-      }
-    }
-    const bool short_pass = short0 && sfs < 12 && (!mixed0 || sfs >= 3);
-    if (short_pass && 3 * (int)g_tab.sfb_short[combo][sfs] >= c1r) {
-      const int pos = C0.scalefac_s[sfs][win];
-      if (pos < 7) {
-        l = l * g_tab.is_ratio[pos][0];
-        r = r * g_tab.is_ratio[pos][1];
-      }
-    }
-  }
+  common::stereo_line(s.desc, h, combo, L, l, r);
 }
 
 // Phase 1: front end.  Items 0..247: butterfly pairs (sb = 1..31, i = 0..7);

@@ -30,6 +30,8 @@ hipError_t upload_tables(const DspTables& tables);
 // v2 = fused/register-blocked production kernel (default).
 constexpr int kVariantV1 = 1;
 constexpr int kVariantV2 = 2;
+// fast mode (MP3G_MODE_FAST): one wave per chunk, reassociated transforms, +-1 LSB
+constexpr int kVariantFast = 3;
 hipError_t launch_granule(int variant, const ChunkDesc* d_chunks, uint32_t n_chunks,
                           const mp3g_granule* d_gran, const int16_t* d_coef,
                           const mp3g_state* d_state_in, mp3g_state* d_state_out, int16_t* d_pcm,

@@ -3,7 +3,7 @@
 // Holds the constant tables (uploaded once per device) and both exact-mode
 // kernels: v1 (granule_exact.hip, the straightforward per-phase version, kept
 // as an on-device cross-check) and v2 (granule_fused.hip, the production
-// kernel).  One TU so both reach g_tab without relocatable device code.
+// kernel), plus the fast-mode kernel v3 (granule_fast.hip, +-1 LSB).  One TU so both reach g_tab without relocatable device code.
 #include <hip/hip_runtime.h>
 
 #include "../../include/mp3g.h"
@@ -14,15 +14,22 @@
 
 namespace mp3g {
 __device__ DspTables g_tab;
+__constant__ FastTables g_fast;
 }  // namespace mp3g
 
+#include "granule_common.hip"
 #include "granule_exact.hip"
 #include "granule_fused.hip"
+#include "granule_fast.hip"
 
 namespace mp3g {
 
 hipError_t upload_tables(const DspTables& tables) {
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_tab), &tables, sizeof(DspTables), 0, hipMemcpyHostToDevice);
+  hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_tab), &tables, sizeof(DspTables), 0, hipMemcpyHostToDevice);
+  if (e != hipSuccess) return e;
+  FastTables fast;
+  build_fast_tables(tables, &fast);
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_fast), &fast, sizeof(FastTables), 0, hipMemcpyHostToDevice);
 }
 
 hipError_t launch_granule(int variant, const ChunkDesc* d_chunks, uint32_t n_chunks,
@@ -30,7 +37,10 @@ hipError_t launch_granule(int variant, const ChunkDesc* d_chunks, uint32_t n_chu
                           const mp3g_state* d_state_in, mp3g_state* d_state_out, int16_t* d_pcm,
                           hipStream_t stream) {
   if (n_chunks == 0) return hipSuccess;
-  if (variant == kVariantV1)
+  if (variant == kVariantFast)
+    hipLaunchKernelGGL(v3::granule_fast_kernel, dim3(n_chunks), dim3(64), 0, stream, d_chunks, d_gran,
+                       d_coef, d_state_in, d_state_out, d_pcm);
+  else if (variant == kVariantV1)
     hipLaunchKernelGGL(v1::granule_exact_kernel, dim3(n_chunks), dim3(256), 0, stream, d_chunks,
                        d_gran, d_coef, d_state_in, d_state_out, d_pcm);
   else

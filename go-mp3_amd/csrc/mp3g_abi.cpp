@@ -174,12 +174,18 @@ int mp3g_plan_create(int device, const mp3g_stream* streams, uint32_t n_streams,
                      uint32_t granules_per_chunk, uint32_t mode, mp3g_plan** out_plan) {
   if (!out_plan || (n_streams && !streams)) return fail(MP3G_ERR_INVALID_ARGUMENT, "null argument");
   *out_plan = nullptr;
-  if ((mode & 0xffu) != MP3G_MODE_EXACT) return fail(MP3G_ERR_UNSUPPORTED, "mode not available");
+  const uint32_t base_mode = mode & 0xffu;
+  if (base_mode != MP3G_MODE_EXACT && base_mode != MP3G_MODE_FAST)
+    return fail(MP3G_ERR_UNSUPPORTED, "mode not available");
   uint64_t total = 0;
   for (uint32_t s = 0; s < n_streams; s++) total += streams[s].n_granules;
   uint32_t k = granules_per_chunk;
-  if (k == 0) {  // automatic: ~2048 workgroups, never fewer than 8 granules each
-    const uint64_t want = (total + 2047) / 2048;
+  if (k == 0) {
+    // automatic.  exact: ~2048 workgroups of 4 waves; fast: ~8192 one-wave
+    // workgroups (11 resident per CU).  Never fewer than 8 granules per chunk
+    // so the 2-granule halo stays <= 25 %.
+    const uint64_t wgs = base_mode == MP3G_MODE_FAST ? 8192 : 2048;
+    const uint64_t want = (total + wgs - 1) / wgs;
     k = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(want, 8), 1u << 20);
   }
   DeviceGuard guard(device);
@@ -263,7 +269,9 @@ int mp3g_plan_execute(mp3g_plan* p, const mp3g_granule* d_gran, const int16_t* d
   for (const ChunkDesc& c : p->chunks) {
     if ((c.flags & kChunkStateOut) && !d_state_out) return fail(MP3G_ERR_INVALID_ARGUMENT, "state_out needed");
   }
-  const int variant = (p->mode & MP3G_FLAG_KERNEL_V1) ? kVariantV1 : kVariantV2;
+  const int variant = (p->mode & 0xffu) == MP3G_MODE_FAST ? kVariantFast
+                      : (p->mode & MP3G_FLAG_KERNEL_V1)      ? kVariantV1
+                                                             : kVariantV2;
   HIP_TRY(launch_granule(variant, p->d_chunks, (uint32_t)p->chunks.size(), d_gran, d_coef, d_state_in,
                          d_state_out, d_pcm, static_cast<hipStream_t>(hip_stream)));
   return MP3G_OK;

@@ -1,0 +1,151 @@
+"""GPU parity of the FAST mode (MP3G_MODE_FAST, granule_fast.hip) vs the oracle.
+
+Bar (BASELINE.json north star): PCM within +-1 LSB int16 of the reference
+Frame.Decode output on the same inputs.  The fast kernel keeps the front end
+(requantize, reorder, stereo) bit-exact and reassociates / FMA-contracts the
+IMDCT, matrixing and window sums, so a sample can differ only where the
+reference's float32 sum sits within a few ulps of an integer boundary of
+sum * 32767.  Besides the +-1 bound the tests pin:
+  * the fraction of differing samples stays tiny (< 1 %),
+  * silence decodes to exact zeros and clipping to exactly +-32767,
+  * the chunk/halo decomposition is bit-identical to a serial fast decode
+    (the halo replays the same float ops), i.e. batch invariance.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from mp3g import synth
+from test_gpu_parity import SYNTH_CASES, run_plan
+
+pytestmark = pytest.mark.gpu
+
+TOL_LSB = 1          # north-star tolerance
+MAX_DIFF_FRAC = 0.01  # differing samples (sanity bound on how often +-1 occurs)
+
+
+def fast_plan(mp3g, g, c, s, chunk=0, state_in=None):
+    return run_plan(mp3g, g, c, s, chunk=chunk, state_in=state_in, mode=mp3g.MODE_FAST)
+
+
+def assert_close(got, want, what):
+    assert got.shape == want.shape, (got.shape, want.shape)
+    d = np.abs(got.astype(np.int32) - want.astype(np.int32))
+    frac = float((d > 0).mean()) if d.size else 0.0
+    assert d.max(initial=0) <= TOL_LSB, f"{what}: max|dPCM|={d.max()} LSB (> {TOL_LSB})"
+    assert frac < MAX_DIFF_FRAC, f"{what}: {frac:.4%} of samples differ"
+    return int(d.max(initial=0)), frac
+
+
+@pytest.mark.parametrize("name", ["classic_lame.mp3", "mpeg2.mp3"])
+def test_fast_sample_files(gpu, captured, name):
+    g, c, want = captured[name]
+    pcm, _ = gpu.decode_host(g, c, mode=gpu.MODE_FAST)
+    assert_close(pcm, want, name)
+
+
+def test_fast_chunking_is_bit_identical(gpu, captured):
+    g, c, want = captured["classic_lame.mp3"]
+    s = gpu.streams_for([len(g)], gpu.STATE_OUT)
+    ref, so_ref = fast_plan(gpu, g, c, s, chunk=len(g))  # one chunk = serial decode
+    assert_close(ref, want, "serial fast")
+    for chunk in (1, 2, 3, 5, 8, 64, 0):
+        pcm, so = fast_plan(gpu, g, c, s, chunk=chunk)
+        assert np.array_equal(pcm, ref), f"chunk={chunk} differs from serial fast decode"
+        assert so.tobytes() == so_ref.tobytes(), f"chunk={chunk}: exported state differs"
+
+
+@pytest.mark.parametrize("case", sorted(SYNTH_CASES))
+def test_fast_synthetic_branches(gpu, case):
+    g, c, s = synth.synth_batch(6, 60, seed=100 + len(case), **SYNTH_CASES[case])
+    want, _ = oracle.dsp_streams(g, c, s)
+    pcm, _ = gpu.decode_host(g, c, s, mode=gpu.MODE_FAST | gpu.FLAG_CHECKED)
+    assert_close(pcm, want, case)
+    for chunk in (1, 4):
+        pcm2, _ = fast_plan(gpu, g, c, s, chunk=chunk)
+        assert np.array_equal(pcm2, pcm), f"{case} chunk={chunk} not batch-invariant"
+
+
+def test_fast_mode_switch_mono_stereo(gpu):
+    parts = [synth.synth_stream(11, 6), synth.synth_stream(12, 20, mode=synth.MODE_MONO),
+             synth.synth_stream(13, 8), synth.synth_stream(14, 3, mode=synth.MODE_MONO),
+             synth.synth_stream(15, 5)]
+    g = np.concatenate([p[0] for p in parts])
+    c = np.concatenate([p[1] for p in parts])
+    s = gpu.streams_for([len(g)], gpu.STATE_OUT)
+    want, _ = oracle.dsp_streams(g, c, s)
+    ref, so_ref = fast_plan(gpu, g, c, s, chunk=len(g))
+    assert_close(ref, want, "switch serial")
+    for chunk in (1, 2, 5, 7, 0):
+        pcm, so = fast_plan(gpu, g, c, s, chunk=chunk)
+        assert np.array_equal(pcm, ref), f"switch chunk={chunk}"
+        assert so.tobytes() == so_ref.tobytes(), f"switch state chunk={chunk}"
+
+
+def test_fast_state_continuation(gpu):
+    """Two calls carrying the state: the exported state holds V rebuilt from its
+    32 distinct values, so the continuation stays within the +-1 bound."""
+    g, c, _ = synth.synth_batch(1, 120, seed=7, p_mixed=0.3)
+    n = len(g)
+    want, so_ref = oracle.dsp_streams(g, c, gpu.streams_for([n], gpu.STATE_OUT))
+    cut = 101
+    p1, st1 = gpu.decode_host(g[:cut], c[:cut], gpu.streams_for([cut], gpu.STATE_OUT), mode=gpu.MODE_FAST)
+    s2 = gpu.streams_for([n - cut], gpu.STATE_IN | gpu.STATE_OUT)
+    p2, st2 = gpu.decode_host(g[cut:], c[cut:], s2, state_in=st1, mode=gpu.MODE_FAST)
+    assert_close(np.concatenate([p1, p2]), want, "continuation")
+    # the overlap store is carried verbatim; compare the state numerically
+    np.testing.assert_allclose(st2["store"], so_ref["store"], rtol=1e-4, atol=1e-4)
+    p3, _ = fast_plan(gpu, g[cut:], c[cut:], s2, chunk=3, state_in=st1)
+    assert np.array_equal(p3, p2), "continuation chunked"
+    # exact state in -> fast decode: still within the bound
+    _, st_exact = oracle.dsp_streams(g[:cut], c[:cut], gpu.streams_for([cut], gpu.STATE_OUT))
+    p4, _ = gpu.decode_host(g[cut:], c[cut:], s2, state_in=st_exact, mode=gpu.MODE_FAST)
+    assert_close(p4, want[cut:], "exact state -> fast")
+
+
+def test_fast_edge_cases(gpu):
+    g, c, s = synth.synth_batch(3, 10, seed=5)
+    g0, c0 = g.copy(), np.zeros_like(c)
+    g0["ch"]["count1"] = 0
+    assert np.all(gpu.decode_host(g0, c0, s, mode=gpu.MODE_FAST)[0] == 0)
+    g1, c1 = g.copy(), c.copy()
+    g1["ch"]["count1"] = 576
+    rng = np.random.default_rng(3)
+    c1[:] = rng.choice(np.array([-8206, -15, 0, 15, 8206], np.int16), size=c1.shape)
+    g1["ch"]["global_gain"] = 255
+    g1["ch"]["scalefac_l"] = 0
+    g1["ch"]["scalefac_s"] = 0
+    want, _ = oracle.dsp_streams(g1, c1, s)
+    pcm, _ = gpu.decode_host(g1, c1, s, mode=gpu.MODE_FAST)
+    assert_close(pcm, want, "full-scale")
+    assert np.abs(pcm).max() == 32767
+    # empty streams with state pass-through
+    st_in = np.zeros(2, gpu.STATE_DTYPE)
+    streams = np.zeros(2, gpu.STREAM_DTYPE)
+    streams["n_granules"] = [0, len(g)]
+    streams["flags"] = [gpu.STATE_IN | gpu.STATE_OUT, gpu.STATE_OUT]
+    pcm, so = gpu.decode_host(g, c, streams, state_in=st_in, mode=gpu.MODE_FAST)
+    want, _ = oracle.dsp_streams(g, c, streams, state_in=st_in)
+    assert_close(pcm, want, "empty streams")
+    assert not so[0]["store"].any() and not so[0]["vvec"].any()
+
+
+def test_fast_c2_full_size(gpu):
+    g, c, s = synth.synth_batch(1, 10000, seed=1)
+    want, _ = oracle.dsp_streams(g, c, s)
+    pcm, _ = fast_plan(gpu, g, c, s)
+    dmax, frac = assert_close(pcm, want, "c2 fast")
+    print(f"c2 fast: max|dPCM|={dmax} LSB, {frac:.5%} of samples differ")
+
+
+def test_fast_c3_shape(gpu):
+    g, c, s = synth.synth_batch(48, 1024, seed=1)
+    want = oracle.dsp_streams_mt(g, c, s, 16)
+    pcm, _ = fast_plan(gpu, g, c, s)
+    assert_close(pcm, want, "c3-shape fast")
+    half = len(g) // 2
+    p_a, _ = fast_plan(gpu, g[:half], c[:half], s[:24])
+    s_b = s[24:].copy()
+    s_b["first_granule"] -= half
+    p_b, _ = fast_plan(gpu, g[half:], c[half:], s_b, chunk=7)
+    assert np.array_equal(np.concatenate([p_a, p_b]), pcm), "c3 fast split batches"
