@@ -72,6 +72,14 @@ struct FastTables {
   float dct[32][16];
   float dwin[32][16];
   float aa_cs[8], aa_ca[8];
+  float is_ratio[8][2];           // [is_pos][ch] (rows 0..6 used)
+  // per (combo, output line L): the line's long band (bits 0..4), short band
+  // (5..8), window of the reorder SOURCE line (9..10), the line's own
+  // window in window-major order (11..12), reorder source line (13..22)
+  uint32_t linfo[kCombos][576];
+  uint16_t sfb_long[kCombos][23];
+  uint16_t sfb_short[kCombos][14];
+  int8_t pretab[22];
 };
 void build_fast_tables(const DspTables& t, FastTables* f);
 

@@ -49,6 +49,9 @@ struct __align__(16) WaveSmem {
   float win[4][36];        // imdctWinData
   float c36t[18][20];      // distinct cosN36 columns, transposed [q][m] (rows padded to 5 x float4)
   float c12t[12][8];       // cosN12 transposed [p][m] (rows padded to 2 x float4)
+  uint32_t linfo[576];     // FastTables::linfo of the current combo
+  int expo[2 * 22 + 2 * 39];  // requantization exponents n4: long bands [ch][sfb], short [ch][sfb][win]
+  float isr[8][2];
   mp3g_granule desc;
 };
 
@@ -112,6 +115,17 @@ __device__ void prologue(const ChunkDesc& cd, const mp3g_granule* gran, uint64_t
   init_in[1] = ch1_from_in ? have_in : ((w == s0) && have_in);
 }
 
+// LDS ordering inside the single-wave workgroup.  A wave's LDS operations
+// complete in issue order, so making one lane's ds_write visible to another
+// lane's later ds_read only needs the COMPILER not to reorder them: no
+// s_waitcnt on the wave's outstanding global loads (the prefetch) or PCM
+// stores, which __syncthreads() would drain every phase.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // X of a V block: X[m] = V[m-16] (m >= 16), -V[48-m] (m < 16).
 __device__ __forceinline__ float x_from_v(const float* v, int m) { return m >= 16 ? v[m - 16] : -v[48 - m]; }
 // V of an X vector (inverse identity; V[16] = 0).
@@ -147,6 +161,8 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, const mp3g_granule* __
     const int q = e / 20, m = e % 20;
     s.c36t[q][m] = m < 18 ? g_fast.c36[m][q] : 0.0f;
   }
+  for (int e = lane; e < 16; e += kLanes) (&s.isr[0][0])[e] = (&g_fast.is_ratio[0][0])[e];
+  int cur_combo = -1;
   for (int e = lane; e < 12 * 8; e += kLanes) {
     const int p = e >> 3, m = e & 7;
     s.c12t[p][m] = m < 6 ? g_fast.cos12[m][p] : 0.0f;
@@ -172,7 +188,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, const mp3g_granule* __
 
   const uint64_t end = cd.out_first + cd.n_out;
   if (w < end) load_granule(s, gran, coef, w);
-  __syncthreads();
+  wave_sync();
 
   for (uint64_t g = w; g < end; g++) {
     const bool out = g >= cd.out_first;
@@ -193,16 +209,98 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, const mp3g_granule* __
       if (lane < 10) pd = reinterpret_cast<const uint4*>(gran + g + 1)[lane];
     }
 
-    // ---- front end: requantize + stereo + antialias, lane = (ch, sb = k) ----
+    // ---- per-granule front-end parameters: band exponents, band thresholds ----
+    if (combo != cur_combo) {  // (uniform; normally once per chunk)
+      for (int e = lane; e < 576; e += kLanes) s.linfo[e] = g_fast.linfo[combo][e];
+      cur_combo = combo;
+    }
+    for (int e = lane; e < 2 * 22 + 2 * 39; e += kLanes) {
+      int c, v;
+      if (e < 44) {
+        c = e >= 22;
+        const int sfb = e - 22 * c;
+        const mp3g_channel& D = s.desc.ch[c];
+        v = (int)D.global_gain - 210 -
+            (D.scalefac_scale ? 4 : 2) * ((int)D.scalefac_l[sfb] + (int)D.preflag * (int)g_fast.pretab[sfb]);
+      } else {
+        const int r0 = e - 44;
+        c = r0 >= 39;
+        const int r = r0 - 39 * c, sfb = r / 3, win = r - 3 * sfb;
+        const mp3g_channel& D = s.desc.ch[c];
+        v = (int)D.global_gain - 210 - 8 * (int)D.subblock_gain[win] -
+            (D.scalefac_scale ? 4 : 2) * (int)D.scalefac_s[sfb][win];
+      }
+      s.expo[e] = v;
+    }
+    const int count1 = C.count1;
+    const bool shortblk = C.win_switch_flag == 1 && C.block_type == 2;
+    const bool mixed = C.mixed_block_flag != 0;
+    int nsfs = 0;  // short bands whose first line lies below count1 (frame.go:229-255 loop bound)
+#pragma unroll
+    for (int b = 0; b < 13; b++) nsfs += 3 * (int)g_fast.sfb_short[combo][b] < count1;
+    wave_sync();
+
+    // ---- front end: requantize (gather through the reorder), lane = (ch, sb = k) ----
     float x[18];
 #pragma unroll
-    for (int j = 0; j < 18; j++) x[j] = act ? common::requant_line(s.a.raw[ch], C, 18 * k + j, combo) : 0.0f;
+    for (int j = 0; j < 18; j++) {
+      const int L = 18 * k + j;
+      const uint32_t info = s.linfo[L];
+      const int sfl = info & 31, sfs = (info >> 5) & 15, wsrc = (info >> 9) & 3, wown = (info >> 11) & 3;
+      const int srcr = info >> 13;
+      const bool longlike = !shortblk || (mixed && L < 36);
+      const bool started = sfs < nsfs;
+      const bool reord = sfs == (mixed ? 3 : 0) || started;
+      const int src = longlike || !reord ? L : srcr;
+      const int win = reord ? wsrc : wown;
+      const int eidx = longlike ? 22 * ch + sfl : 44 + 39 * ch + 3 * sfs + win;
+      const bool process = longlike ? (shortblk || L < count1) : started;
+      const int xi = s.a.raw[ch][src];
+      const int n4 = s.expo[eidx];
+      const float mag = ldexpf(g_tab.req[n4 & 3][min(abs(xi), 8206)], n4 >> 2);
+      const float v = xi < 0 ? -mag : mag;
+      x[j] = !act ? 0.0f : (process ? v : (float)xi);
+    }
+    // ---- MS / intensity stereo with the partner channel's lane (frame.go:304-420) ----
     if (nch == 2 && hdr_mode(h) == 1 && (h & 0x30u)) {
+      const mp3g_channel& C0 = s.desc.ch[0];
+      const int c1r = s.desc.ch[1].count1;
+      const int msmax = max((int)C0.count1, c1r);
+      const bool ms = h & 0x20u, is = h & 0x10u;
+      const bool short0 = C0.win_switch_flag == 1 && C0.block_type == 2;
+      const bool mixed0 = C0.mixed_block_flag != 0;
+      int nl_is = 0, ns_is = 0;  // first long / short band starting at or above channel 1's count1
+#pragma unroll
+      for (int b = 0; b < 23; b++) nl_is += (int)g_fast.sfb_long[combo][b] < c1r;
+#pragma unroll
+      for (int b = 0; b < 14; b++) ns_is += 3 * (int)g_fast.sfb_short[combo][b] < c1r;
+      const float inv_sqrt2 = 0.70710678118654752440f;
 #pragma unroll
       for (int j = 0; j < 18; j++) {
+        const int L = 18 * k + j;
         const float o = __shfl_xor(x[j], 32);
         float l = ch ? o : x[j], r = ch ? x[j] : o;
-        common::stereo_line(s.desc, h, combo, 18 * k + j, l, r);
+        if (ms && L < msmax) {
+          const float nl = (l + r) * inv_sqrt2, nr = (l - r) * inv_sqrt2;
+          l = nl;
+          r = nr;
+        }
+        if (is) {
+          const uint32_t info = s.linfo[L];
+          const int sfl = info & 31, sfs = (info >> 5) & 15, wown = (info >> 11) & 3;
+          const bool lp = (!short0 ? (sfl < 21) : (mixed0 && sfl < 8)) && sfl >= nl_is;
+          const int pl = lp ? (int)C0.scalefac_l[sfl] : 7;
+          if (pl < 7) {
+            l = l * s.isr[pl][0];
+            r = r * s.isr[pl][1];
+          }
+          const bool sp = short0 && sfs < 12 && (!mixed0 || sfs >= 3) && sfs >= ns_is;
+          const int ps = sp ? (int)C0.scalefac_s[sfs][wown] : 7;
+          if (ps < 7) {
+            l = l * s.isr[ps][0];
+            r = r * s.isr[ps][1];
+          }
+        }
         x[j] = ch ? r : l;
       }
     }
@@ -282,7 +380,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, const mp3g_granule* __
         if ((k & 1) && (j & 1)) o[j] = -o[j];
       }
     }
-    __syncthreads();  // raw[] fully consumed before eo[] (same LDS) is written
+    wave_sync();  // raw[] fully consumed before eo[] (same LDS) is written
 
     // ---- even/odd fold of S across the subband pair (k, 31-k) ----
 #pragma unroll
@@ -290,7 +388,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, const mp3g_granule* __
       const float oth = __shfl_xor(o[j], 31);
       if (act) s.a.eo[ch][j][k < 16 ? k : 47 - k] = k < 16 ? o[j] + oth : oth - o[j];
     }
-    __syncthreads();
+    wave_sync();
 
     // ---- matrixing: X_k for the 18 slots of this granule ----
     bool need_v = true;
@@ -312,7 +410,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, const mp3g_granule* __
         s.ring[ch][16 + ss][k] = acc;
       }
     }
-    __syncthreads();
+    wave_sync();
 
     // ---- 16-tap window over the X ring -> s16 PCM ----
     if (out && act) {
@@ -348,7 +446,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, const mp3g_granule* __
         }
       }
     }
-    __syncthreads();  // ring reads done
+    wave_sync();  // ring reads done
 
     // ---- history shift (channels this granule touched) + next granule in ----
     for (int e = lane; e < nch * 128; e += kLanes) {
@@ -362,7 +460,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, const mp3g_granule* __
       if (lane < 16) dst[lane + 128] = p2;
       if (lane < 10) reinterpret_cast<uint4*>(&s.desc)[lane] = pd;
     }
-    __syncthreads();
+    wave_sync();
   }
 
   if (cd.flags & kChunkStateOut) {
