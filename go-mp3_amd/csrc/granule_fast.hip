@@ -27,6 +27,7 @@
 // windows) -> 11 resident waves per CU.
 // (compiled as part of kernels.hip, after granule_common.hip)
 #pragma clang fp contract(fast)
+#include "xlane.h"
 
 namespace mp3g {
 namespace v3 {
@@ -38,6 +39,8 @@ using common::hdr_nch;
 using common::pcm_sample;
 
 constexpr int kLanes = 64;
+// pretab[22] (frame.go:39) packed 2 bits per band: no per-lane table load
+__device__ __forceinline__ int kPretab(int sfb) { return (int)((0x2fe95400000ull >> (2 * sfb)) & 3u); }
 constexpr int kRing = 34;  // X slots: 0..15 history (slot 15 newest), 16..33 current granule
 
 struct __align__(16) WaveSmem {
@@ -126,6 +129,27 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Branch-free selects (v_bfi_b32 / v_cndmask): keeps the compiler from turning
+// a per-lane choice between two cheap values into exec-mask branches.
+__device__ __forceinline__ float self(bool c, float a, float b) {
+  const int m = -(int)c;
+  return __int_as_float((__float_as_int(a) & m) | (__float_as_int(b) & ~m));
+}
+__device__ __forceinline__ int seli(bool c, int a, int b) {
+  const int m = -(int)c;
+  return (a & m) | (b & ~m);
+}
+
+// |x|^(4/3) * 2^(n4/4) = ldexp(|x| * 2^(log2|x| / 3 + (n4 & 3) / 4), n4 >> 2), signed:
+// two transcendental VALU ops instead of the float64 table gather of the
+// reference (frame.go:148-155); relative error ~1e-6 (x = 0 -> exactly 0).
+__device__ __forceinline__ float requant_fast(int xi, int n4) {
+  const float ax = (float)abs(xi);
+  const float t = __builtin_amdgcn_logf(ax) * (1.0f / 3.0f) + 0.25f * (float)(n4 & 3);
+  const float mag = ldexpf(ax * __builtin_amdgcn_exp2f(t), n4 >> 2);
+  return xi < 0 ? -mag : mag;
+}
+
 // X of a V block: X[m] = V[m-16] (m >= 16), -V[48-m] (m < 16).
 __device__ __forceinline__ float x_from_v(const float* v, int m) { return m >= 16 ? v[m - 16] : -v[48 - m]; }
 // V of an X vector (inverse identity; V[16] = 0).
@@ -138,10 +162,23 @@ __device__ __forceinline__ float v_from_x(const float* x, int i) {
 
 }  // namespace
 
+// kStamp: diagnostic build -- per-phase s_memtime cycle sums of every wave go
+// to `stamps` (kPhases per workgroup); never used for output.
+constexpr int kPhases = 8;
+template <bool kStamp>
 __global__ void __launch_bounds__(kLanes, 2)
 granule_fast_kernel(const ChunkDesc* __restrict__ chunks, const mp3g_granule* __restrict__ gran,
                     const int16_t* __restrict__ coef, const mp3g_state* __restrict__ state_in,
-                    mp3g_state* __restrict__ state_out, int16_t* __restrict__ pcm) {
+                    mp3g_state* __restrict__ state_out, int16_t* __restrict__ pcm,
+                    unsigned long long* __restrict__ stamps) {
+  unsigned long long ph[kPhases] = {}, tprev = 0;
+  auto stamp = [&](int p) {
+    if constexpr (kStamp) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      ph[p] += t - tprev;
+      tprev = t;
+    }
+  };
   __shared__ WaveSmem s;
   const ChunkDesc cd = chunks[blockIdx.x];
   const int lane = threadIdx.x;
@@ -190,6 +227,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, const mp3g_granule* __
   if (w < end) load_granule(s, gran, coef, w);
   wave_sync();
 
+  if constexpr (kStamp) tprev = __builtin_amdgcn_s_memtime();
   for (uint64_t g = w; g < end; g++) {
     const bool out = g >= cd.out_first;
     const uint32_t h = s.desc.header;
@@ -221,7 +259,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, const mp3g_granule* __
         const int sfb = e - 22 * c;
         const mp3g_channel& D = s.desc.ch[c];
         v = (int)D.global_gain - 210 -
-            (D.scalefac_scale ? 4 : 2) * ((int)D.scalefac_l[sfb] + (int)D.preflag * (int)g_fast.pretab[sfb]);
+            (D.scalefac_scale ? 4 : 2) * ((int)D.scalefac_l[sfb] + (int)D.preflag * kPretab(sfb));
       } else {
         const int r0 = e - 44;
         c = r0 >= 39;
@@ -239,28 +277,62 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, const mp3g_granule* __
 #pragma unroll
     for (int b = 0; b < 13; b++) nsfs += 3 * (int)g_fast.sfb_short[combo][b] < count1;
     wave_sync();
+    stamp(0);
 
     // ---- front end: requantize (gather through the reorder), lane = (ch, sb = k) ----
+    // the lane's 18 line-info words and raw integers are loaded in bulk first
     float x[18];
+    uint32_t info[18];
+    {
+      const uint2* li = reinterpret_cast<const uint2*>(&s.linfo[18 * k]);
 #pragma unroll
-    for (int j = 0; j < 18; j++) {
-      const int L = 18 * k + j;
-      const uint32_t info = s.linfo[L];
-      const int sfl = info & 31, sfs = (info >> 5) & 15, wsrc = (info >> 9) & 3, wown = (info >> 11) & 3;
-      const int srcr = info >> 13;
-      const bool longlike = !shortblk || (mixed && L < 36);
-      const bool started = sfs < nsfs;
-      const bool reord = sfs == (mixed ? 3 : 0) || started;
-      const int src = longlike || !reord ? L : srcr;
-      const int win = reord ? wsrc : wown;
-      const int eidx = longlike ? 22 * ch + sfl : 44 + 39 * ch + 3 * sfs + win;
-      const bool process = longlike ? (shortblk || L < count1) : started;
-      const int xi = s.a.raw[ch][src];
-      const int n4 = s.expo[eidx];
-      const float mag = ldexpf(g_tab.req[n4 & 3][min(abs(xi), 8206)], n4 >> 2);
-      const float v = xi < 0 ? -mag : mag;
-      x[j] = !act ? 0.0f : (process ? v : (float)xi);
+      for (int q = 0; q < 9; q++) {
+        const uint2 v = li[q];
+        info[2 * q] = v.x;
+        info[2 * q + 1] = v.y;
+      }
     }
+    // wave-uniform: every channel of this granule is a long block (no reorder)
+    const bool all_long = __builtin_amdgcn_readfirstlane(
+        !(s.desc.ch[0].win_switch_flag == 1 && s.desc.ch[0].block_type == 2) &&
+        (nch == 1 || !(s.desc.ch[1].win_switch_flag == 1 && s.desc.ch[1].block_type == 2)));
+    if (all_long) {
+      int xi[18];
+      const uint32_t* rw = reinterpret_cast<const uint32_t*>(&s.a.raw[ch][18 * k]);
+#pragma unroll
+      for (int q = 0; q < 9; q++) {
+        const uint32_t w = rw[q];
+        xi[2 * q] = (int)(int16_t)(w & 0xffffu);
+        xi[2 * q + 1] = (int)(int16_t)(w >> 16);
+      }
+      int n4[18];
+#pragma unroll
+      for (int j = 0; j < 18; j++) n4[j] = s.expo[22 * ch + (info[j] & 31)];
+#pragma unroll
+      for (int j = 0; j < 18; j++) {
+        // (absent-channel lanes compute garbage that nothing reads)
+        x[j] = self(18 * k + j < count1, requant_fast(xi[j], n4[j]), (float)xi[j]);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 18; j++) {
+        const int L = 18 * k + j;
+        const uint32_t inf = info[j];
+        const int sfl = inf & 31, sfs = (inf >> 5) & 15, wsrc = (inf >> 9) & 3, wown = (inf >> 11) & 3;
+        const int srcr = inf >> 13;
+        const bool longlike = !shortblk || (mixed && L < 36);
+        const bool started = sfs < nsfs;
+        const bool reord = sfs == (mixed ? 3 : 0) || started;
+        const int src = seli(longlike || !reord, L, srcr);
+        const int win = seli(reord, wsrc, wown);
+        const int eidx = seli(longlike, 22 * ch + sfl, 44 + 39 * ch + 3 * sfs + win);
+        const bool process = longlike ? (shortblk || L < count1) : started;
+        const int xi = s.a.raw[ch][src];
+        const int n4 = s.expo[eidx];
+        x[j] = self(process, requant_fast(xi, n4), (float)xi);
+      }
+    }
+    stamp(1);
     // ---- MS / intensity stereo with the partner channel's lane (frame.go:304-420) ----
     if (nch == 2 && hdr_mode(h) == 1 && (h & 0x30u)) {
       const mp3g_channel& C0 = s.desc.ch[0];
@@ -275,33 +347,37 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, const mp3g_granule* __
 #pragma unroll
       for (int b = 0; b < 14; b++) ns_is += 3 * (int)g_fast.sfb_short[combo][b] < c1r;
       const float inv_sqrt2 = 0.70710678118654752440f;
+      if (!is) {  // MS only (the common joint-stereo case): L' = (l+r)c, R' = (l-r)c
+        const float sg = ch ? -1.0f : 1.0f;
+#pragma unroll
+        for (int j = 0; j < 18; j++) {
+          const float o = xl::xor32(x[j]);
+          const float m = (o + sg * x[j]) * inv_sqrt2;
+          x[j] = 18 * k + j < msmax ? m : x[j];
+        }
+      } else
 #pragma unroll
       for (int j = 0; j < 18; j++) {
         const int L = 18 * k + j;
-        const float o = __shfl_xor(x[j], 32);
-        float l = ch ? o : x[j], r = ch ? x[j] : o;
-        if (ms && L < msmax) {
-          const float nl = (l + r) * inv_sqrt2, nr = (l - r) * inv_sqrt2;
-          l = nl;
-          r = nr;
-        }
+        const float o = xl::xor32(x[j]);
+        float l = self(ch, o, x[j]), r = self(ch, x[j], o);
+        const bool msl = ms && L < msmax;
+        const float nl = (l + r) * inv_sqrt2, nr = (l - r) * inv_sqrt2;
+        l = self(msl, nl, l);
+        r = self(msl, nr, r);
         if (is) {
           const uint32_t info = s.linfo[L];
           const int sfl = info & 31, sfs = (info >> 5) & 15, wown = (info >> 11) & 3;
           const bool lp = (!short0 ? (sfl < 21) : (mixed0 && sfl < 8)) && sfl >= nl_is;
-          const int pl = lp ? (int)C0.scalefac_l[sfl] : 7;
-          if (pl < 7) {
-            l = l * s.isr[pl][0];
-            r = r * s.isr[pl][1];
-          }
+          const int pl = seli(lp, (int)C0.scalefac_l[min(sfl, 21)], 7);
+          l = self(pl < 7, l * s.isr[min(pl, 7)][0], l);
+          r = self(pl < 7, r * s.isr[min(pl, 7)][1], r);
           const bool sp = short0 && sfs < 12 && (!mixed0 || sfs >= 3) && sfs >= ns_is;
-          const int ps = sp ? (int)C0.scalefac_s[sfs][wown] : 7;
-          if (ps < 7) {
-            l = l * s.isr[ps][0];
-            r = r * s.isr[ps][1];
-          }
+          const int ps = seli(sp, (int)C0.scalefac_s[min(sfs, 12)][min(wown, 2)], 7);
+          l = self(ps < 7, l * s.isr[min(ps, 7)][0], l);
+          r = self(ps < 7, r * s.isr[min(ps, 7)][1], r);
         }
-        x[j] = ch ? r : l;
+        x[j] = self(ch, r, l);
       }
     }
     {
@@ -313,18 +389,19 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, const mp3g_granule* __
       float up[8], dn[8];
 #pragma unroll
       for (int i = 0; i < 8; i++) {
-        up[i] = __shfl_up(x[17 - i], 1);  // x_{k-1}[17-i]
-        dn[i] = __shfl_down(x[i], 1);     // x_{k+1}[i]
+        up[i] = xl::from_prev(x[17 - i]);  // x_{k-1}[17-i]
+        dn[i] = xl::from_next(x[i]);       // x_{k+1}[i]
       }
 #pragma unroll
       for (int i = 0; i < 8; i++) {
         const float cs = g_fast.aa_cs[i], ca = g_fast.aa_ca[i];
         const float ui = x[i], li = x[17 - i];
-        if (lower) x[i] = ui * cs + up[i] * ca;
-        if (upper) x[17 - i] = li * cs - dn[i] * ca;
+        x[i] = self(lower, ui * cs + up[i] * ca, ui);
+        x[17 - i] = self(upper, li * cs - dn[i] * ca, li);
       }
     }
 
+    stamp(2);
     // ---- IMDCT + overlap + frequency inversion ----
     float o[18];
     {
@@ -376,26 +453,28 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, const mp3g_granule* __
 #pragma unroll
       for (int j = 0; j < 18; j++) {
         o[j] = r[j] + st[j];
-        if (act) st[j] = r[18 + j];
-        if ((k & 1) && (j & 1)) o[j] = -o[j];
+        st[j] = self(act, r[18 + j], st[j]);
+        if (j & 1) o[j] = self(k & 1, -o[j], o[j]);
       }
     }
     wave_sync();  // raw[] fully consumed before eo[] (same LDS) is written
+    stamp(3);
 
     // ---- even/odd fold of S across the subband pair (k, 31-k) ----
 #pragma unroll
     for (int j = 0; j < 18; j++) {
-      const float oth = __shfl_xor(o[j], 31);
+      const float oth = xl::xor31(o[j]);
       if (act) s.a.eo[ch][j][k < 16 ? k : 47 - k] = k < 16 ? o[j] + oth : oth - o[j];
     }
     wave_sync();
+    stamp(4);
 
     // ---- matrixing: X_k for the 18 slots of this granule ----
     bool need_v = true;
     if (!out && g + 1 < cd.out_first) need_v = hdr_nch(gran[g + 1].header) < nch;
     if (need_v && act) {
       const float* E = &s.a.eo[ch][0][(k & 1) * 16];
-#pragma unroll 2
+#pragma unroll 6
       for (int ss = 0; ss < 18; ss++) {
         const float4* e4 = reinterpret_cast<const float4*>(E + 32 * ss);
         float acc = 0.0f;
@@ -411,6 +490,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, const mp3g_granule* __
       }
     }
     wave_sync();
+    stamp(5);
 
     // ---- 16-tap window over the X ring -> s16 PCM ----
     if (out && act) {
@@ -433,7 +513,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, const mp3g_granule* __
 #pragma unroll
         for (int q = 0; q < 9; q++) {
           const int a = pcm_sample(acc[2 * q]), b = pcm_sample(acc[2 * q + 1]);
-          const int got = __shfl_xor(ch ? a : b, 32);
+          const int got = xl::xor32i(ch ? a : b);
           // lane (0,k) stores slot 2q, lane (1,k) slot 2q+1: (L, R) = low, high half
           const int L = ch ? got : a, Rr = ch ? b : got;
           dst[32 * (2 * q + ch) + k] = (uint32_t)(L & 0xffff) | ((uint32_t)Rr << 16);
@@ -447,6 +527,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, const mp3g_granule* __
       }
     }
     wave_sync();  // ring reads done
+    stamp(6);
 
     // ---- history shift (channels this granule touched) + next granule in ----
     for (int e = lane; e < nch * 128; e += kLanes) {
@@ -461,6 +542,11 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, const mp3g_granule* __
       if (lane < 10) reinterpret_cast<uint4*>(&s.desc)[lane] = pd;
     }
     wave_sync();
+    stamp(7);
+  }
+  if constexpr (kStamp) {
+    if (threadIdx.x == 0)
+      for (int p = 0; p < kPhases; p++) stamps[(size_t)blockIdx.x * kPhases + p] = ph[p];
   }
 
   if (cd.flags & kChunkStateOut) {

@@ -37,4 +37,10 @@ hipError_t launch_granule(int variant, const ChunkDesc* d_chunks, uint32_t n_chu
                           const mp3g_state* d_state_in, mp3g_state* d_state_out, int16_t* d_pcm,
                           hipStream_t stream);
 
+// Diagnostic: fast kernel with per-phase s_memtime sums (8 per chunk) in d_stamps.
+constexpr int kFastPhases = 8;
+hipError_t launch_fast_stamped(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_granule* d_gran,
+                               const int16_t* d_coef, const mp3g_state* d_state_in, mp3g_state* d_state_out,
+                               int16_t* d_pcm, unsigned long long* d_stamps, hipStream_t stream);
+
 }  // namespace mp3g

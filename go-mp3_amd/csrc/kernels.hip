@@ -3,7 +3,8 @@
 // Holds the constant tables (uploaded once per device) and both exact-mode
 // kernels: v1 (granule_exact.hip, the straightforward per-phase version, kept
 // as an on-device cross-check) and v2 (granule_fused.hip, the production
-// kernel), plus the fast-mode kernel v3 (granule_fast.hip, +-1 LSB).  One TU so both reach g_tab without relocatable device code.
+// kernel), plus the fast-mode kernel v3 (granule_fast.hip, +-1 LSB).  One TU
+// so all of them reach g_tab / g_fast without relocatable device code.
 #include <hip/hip_runtime.h>
 
 #include "../../include/mp3g.h"
@@ -38,14 +39,23 @@ hipError_t launch_granule(int variant, const ChunkDesc* d_chunks, uint32_t n_chu
                           hipStream_t stream) {
   if (n_chunks == 0) return hipSuccess;
   if (variant == kVariantFast)
-    hipLaunchKernelGGL(v3::granule_fast_kernel, dim3(n_chunks), dim3(64), 0, stream, d_chunks, d_gran,
-                       d_coef, d_state_in, d_state_out, d_pcm);
+    hipLaunchKernelGGL(v3::granule_fast_kernel<false>, dim3(n_chunks), dim3(64), 0, stream, d_chunks, d_gran,
+                       d_coef, d_state_in, d_state_out, d_pcm, nullptr);
   else if (variant == kVariantV1)
     hipLaunchKernelGGL(v1::granule_exact_kernel, dim3(n_chunks), dim3(256), 0, stream, d_chunks,
                        d_gran, d_coef, d_state_in, d_state_out, d_pcm);
   else
     hipLaunchKernelGGL(v2::granule_fused_kernel, dim3(n_chunks), dim3(256), 0, stream, d_chunks,
                        d_gran, d_coef, d_state_in, d_state_out, d_pcm);
+  return hipGetLastError();
+}
+
+hipError_t launch_fast_stamped(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_granule* d_gran,
+                               const int16_t* d_coef, const mp3g_state* d_state_in, mp3g_state* d_state_out,
+                               int16_t* d_pcm, unsigned long long* d_stamps, hipStream_t stream) {
+  if (n_chunks == 0) return hipSuccess;
+  hipLaunchKernelGGL(v3::granule_fast_kernel<true>, dim3(n_chunks), dim3(64), 0, stream, d_chunks, d_gran, d_coef,
+                     d_state_in, d_state_out, d_pcm, d_stamps);
   return hipGetLastError();
 }
 

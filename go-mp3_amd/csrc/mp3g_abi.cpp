@@ -277,6 +277,31 @@ int mp3g_plan_execute(mp3g_plan* p, const mp3g_granule* d_gran, const int16_t* d
   return MP3G_OK;
 }
 
+int mp3g_plan_debug_phases(mp3g_plan* p, const mp3g_granule* d_gran, const int16_t* d_coef, int16_t* d_pcm,
+                           uint64_t* out_cycles, void* hip_stream) {
+  if (!p || !out_cycles) return fail(MP3G_ERR_INVALID_ARGUMENT, "null argument");
+  if ((p->mode & 0xffu) != MP3G_MODE_FAST) return fail(MP3G_ERR_INVALID_ARGUMENT, "not a fast-mode plan");
+  for (int i = 0; i < kFastPhases; i++) out_cycles[i] = 0;
+  if (p->chunks.empty()) return MP3G_OK;
+  for (const ChunkDesc& c : p->chunks)
+    if (c.flags & (kChunkStateIn | kChunkStateOut)) return fail(MP3G_ERR_INVALID_ARGUMENT, "stateful plan");
+  DeviceGuard guard(p->device);
+  if (guard.err != hipSuccess) return fail(MP3G_ERR_NO_DEVICE, "hipSetDevice", guard.err);
+  const size_t n = p->chunks.size() * kFastPhases;
+  unsigned long long* d_st = nullptr;
+  hipError_t e = hipMalloc(&d_st, n * sizeof(unsigned long long));
+  if (e != hipSuccess) return fail(MP3G_ERR_OUT_OF_MEMORY, "hipMalloc(stamps)", e);
+  hipStream_t st = static_cast<hipStream_t>(hip_stream);
+  e = launch_fast_stamped(p->d_chunks, (uint32_t)p->chunks.size(), d_gran, d_coef, nullptr, nullptr, d_pcm, d_st, st);
+  std::vector<unsigned long long> h(n);
+  if (e == hipSuccess) e = hipMemcpyAsync(h.data(), d_st, n * sizeof(unsigned long long), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  (void)hipFree(d_st);
+  if (e != hipSuccess) return fail(MP3G_ERR_DEVICE, "stamped launch", e);
+  for (size_t i = 0; i < n; i++) out_cycles[i % kFastPhases] += h[i];
+  return MP3G_OK;
+}
+
 int mp3g_decode_host(int device, const mp3g_granule* granules, const int16_t* coeffs,
                      uint64_t n_granules, const mp3g_stream* streams, uint32_t n_streams,
                      const mp3g_state* state_in, mp3g_state* state_out, int16_t* pcm,

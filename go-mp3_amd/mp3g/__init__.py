@@ -69,6 +69,7 @@ def lib():
         L.mp3g_plan_info.argtypes = [vp, C.POINTER(u64), C.POINTER(u64), C.POINTER(u64)]
         L.mp3g_plan_execute.argtypes = [vp, vp, vp, vp, vp, vp, vp]
         L.mp3g_decode_host.argtypes = [C.c_int, vp, vp, u64, vp, u32, vp, vp, vp, u32]
+        L.mp3g_plan_debug_phases.argtypes = [vp, vp, vp, vp, C.POINTER(u64), vp]
         _lib = L
     return _lib
 
@@ -154,6 +155,17 @@ class Plan:
         _check(lib().mp3g_plan_execute(self._h, p(d_gran), p(d_coef), p(d_state_in),
                                        p(d_state_out), p(d_pcm),
                                        C.c_void_p(stream) if stream else None))
+
+    PHASES = ("params", "requantize", "stereo+antialias", "imdct", "eo-fold", "matrixing",
+              "window+store", "history")
+
+    def debug_phases(self, d_gran, d_coef, d_pcm, stream=None):
+        """Diagnostic (fast plans): summed shader cycles per kernel phase."""
+        out = (C.c_uint64 * 8)()
+        p = lambda x: C.c_void_p(x.data_ptr() if hasattr(x, "data_ptr") else int(x))
+        _check(lib().mp3g_plan_debug_phases(self._h, p(d_gran), p(d_coef), p(d_pcm), out,
+                                            C.c_void_p(stream) if stream else None))
+        return dict(zip(self.PHASES, list(out)))
 
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:

@@ -119,9 +119,9 @@ def test_exact_kernel_has_no_fma():
     kernels = re.findall(r"^(_ZN4mp3g2v\d\w+kernel\w*):(.*?)\.end_amdhsa_kernel", asm, re.S | re.M)
     exact = [(n, b) for n, b in kernels if "granule_fast" not in n]
     fast = [(n, b) for n, b in kernels if "granule_fast" in n]
-    assert len(exact) >= 2 and len(fast) == 1, [k[0] for k in kernels]
+    assert len(exact) >= 2 and len(fast) >= 1, [k[0] for k in kernels]
     # the fast kernel (+-1 LSB mode) is the one allowed -- and expected -- to contract
-    assert re.search(r"\bv_(pk_)?fmac?_f32", fast[0][1]), "fast kernel lost its FMAs"
+    assert all(re.search(r"\bv_(pk_)?fmac?_f32", b) for _, b in fast), "fast kernel lost its FMAs"
     for name, body in exact:
         assert "v_mul_f32" in body and "v_add_f32" in body, name
         bad = re.findall(r"\b(v_fma\w*|v_fmac\w*|v_mac_\w*|v_mad_\w*f32|v_pk_fma\w*)\b", body)
