@@ -77,6 +77,9 @@ struct FastTables {
   // (5..8), window of the reorder SOURCE line (9..10), the line's own
   // window in window-major order (11..12), reorder source line (13..22)
   uint32_t linfo[kCombos][576];
+  // per (combo, subband): long band of the subband's first line (bits 0..4)
+  // and a mask of the lines j = 1..17 that start a new long band (bits 5+j)
+  uint32_t lband[kCombos][32];
   uint16_t sfb_long[kCombos][23];
   uint16_t sfb_short[kCombos][14];
   int8_t pretab[22];

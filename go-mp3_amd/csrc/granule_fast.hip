@@ -31,36 +31,56 @@
 
 namespace mp3g {
 namespace v3 {
+constexpr int kWaves = 4;  // independent chunks (one per wave) per workgroup; they share the tables
 namespace {
 
 using common::hdr_combo;
 using common::hdr_mode;
 using common::hdr_nch;
-using common::pcm_sample;
+// int(sum * 32767) clamped to +-32767 (frame.go:663-669).  The exact kernels
+// also reproduce Go's result for NaN / |t| >= 2^63; no decodable input gets
+// near that (|sum| < 1e12), so the fast path is clamp + truncate.
+__device__ __forceinline__ int pcm_sample(float sum) {
+  return (int)__builtin_amdgcn_fmed3f(sum * 32767.0f, -32767.0f, 32767.0f);
+}
 
 constexpr int kLanes = 64;
+// Packed FP32: one v_pk_fma_f32 does two FMAs in the issue slot of one
+// v_fma_f32 (measured on MI355X: 122 vs 51-69 TFLOP/s, tools/valu_bench.hip),
+// so the IMDCT, matrixing and window sums are written on float pairs.
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 pfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2 bcast(float v) { return (f2){v, v}; }
 // pretab[22] (frame.go:39) packed 2 bits per band: no per-lane table load
 __device__ __forceinline__ int kPretab(int sfb) { return (int)((0x2fe95400000ull >> (2 * sfb)) & 3u); }
-constexpr int kRing = 34;  // X slots: 0..15 history (slot 15 newest), 16..33 current granule
+// X ring slots: 0..14 history (slot 14 newest), 15..32 the current granule.
+// The window of slot ss reads slots 15+ss-j, j = 0..15, so 15 history slots
+// suffice (the 16th V block of Frame.vVec is never read again).
+constexpr int kHist = 15;
+constexpr int kRing = kHist + 18;
 
+// read-only tables, one copy per workgroup
+struct __align__(16) SharedSmem {
+  float win[4][36];    // imdctWinData
+  f2 c36p[9][18];      // distinct cosN36 columns as pairs (col q, col 18+q): [q][m]
+  float c12t[12][8];   // cosN12 transposed [p][m] (rows padded to 2 x float4)
+  float isr[8][2];
+  float dct[32][20];   // FastTables::dct rows (padded: conflict-free b128 row reads)
+  float dwin[32][20];  // FastTables::dwin rows
+};
+// per-wave working set: 11.4 KB -> 3 workgroups (12 waves) per CU
 struct __align__(16) WaveSmem {
   union {
-    int16_t raw[2][576];   // Huffman integers of the current granule
-    float eo[2][18][32];   // folded matrixing input [ch][slot][k]: even part k<16, odd part 16+k
+    int16_t raw[2][576];  // Huffman integers of the current granule
+    f2 eo[2][3][32];      // folded matrixing input of 6 slots [ch][slot pair][k]: even k<16, odd 16+k
   } a;
   float ring[2][kRing][32];
-  float win[4][36];        // imdctWinData
-  float c36t[18][20];      // distinct cosN36 columns, transposed [q][m] (rows padded to 5 x float4)
-  float c12t[12][8];       // cosN12 transposed [p][m] (rows padded to 2 x float4)
-  uint32_t linfo[576];     // FastTables::linfo of the current combo
   int expo[2 * 22 + 2 * 39];  // requantization exponents n4: long bands [ch][sfb], short [ch][sfb][win]
-  float isr[8][2];
   mp3g_granule desc;
 };
 
 __device__ __forceinline__ void load_granule(WaveSmem& s, const mp3g_granule* gran, const int16_t* coef,
-                                             uint64_t g) {
-  const int t = threadIdx.x;
+                                             uint64_t g, int t) {
   const uint4* src = reinterpret_cast<const uint4*>(coef + g * MP3G_COEF_PER_GRANULE);
   uint4* dst = reinterpret_cast<uint4*>(&s.a.raw[0][0]);
   dst[t] = src[t];
@@ -71,7 +91,8 @@ __device__ __forceinline__ void load_granule(WaveSmem& s, const mp3g_granule* gr
 
 // Replay start of a chunk (same decision as v2::plan_prologue, with wave
 // ballots instead of a workgroup scan).
-__device__ void prologue(const ChunkDesc& cd, const mp3g_granule* gran, uint64_t* w_out, int init_in[2]) {
+__device__ void prologue(const ChunkDesc& cd, const mp3g_granule* gran, uint64_t* w_out, int init_in[2],
+                         int lane) {
   const uint64_t c0 = cd.out_first, s0 = cd.stream_first;
   const bool have_in = cd.flags & kChunkStateIn;
   if (c0 == s0) {
@@ -88,7 +109,7 @@ __device__ void prologue(const ChunkDesc& cd, const mp3g_granule* gran, uint64_t
     return;
   }
   int any = 0;
-  for (uint32_t k = threadIdx.x; k < cd.n_out; k += kLanes) any |= hdr_nch(gran[c0 + k].header) == 2;
+  for (uint32_t k = lane; k < cd.n_out; k += kLanes) any |= hdr_nch(gran[c0 + k].header) == 2;
   const bool need1 = __ballot(any) != 0 || (cd.flags & kChunkStateOut);
   uint64_t start1 = c0;
   bool ch1_from_in = false;
@@ -97,8 +118,8 @@ __device__ void prologue(const ChunkDesc& cd, const mp3g_granule* gran, uint64_t
     uint64_t p2 = 0;
     for (uint64_t hi = c0; hi > s0 && found < 2;) {
       const uint64_t lo = hi - s0 > kLanes ? hi - kLanes : s0;
-      const uint64_t g = hi - 1 - threadIdx.x;
-      const bool stereo = (threadIdx.x < hi - lo) && hdr_nch(gran[g].header) == 2;
+      const uint64_t g = hi - 1 - lane;
+      const bool stereo = ((uint64_t)lane < hi - lo) && hdr_nch(gran[g].header) == 2;
       uint64_t m = __ballot(stereo);
       while (m && found < 2) {
         const int b = __ffsll((unsigned long long)m) - 1;
@@ -166,8 +187,8 @@ __device__ __forceinline__ float v_from_x(const float* x, int i) {
 // to `stamps` (kPhases per workgroup); never used for output.
 constexpr int kPhases = 8;
 template <bool kStamp>
-__global__ void __launch_bounds__(kLanes, 2)
-granule_fast_kernel(const ChunkDesc* __restrict__ chunks, const mp3g_granule* __restrict__ gran,
+__global__ void __launch_bounds__(kLanes * kWaves, 3)
+granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, const mp3g_granule* __restrict__ gran,
                     const int16_t* __restrict__ coef, const mp3g_state* __restrict__ state_in,
                     mp3g_state* __restrict__ state_out, int16_t* __restrict__ pcm,
                     unsigned long long* __restrict__ stamps) {
@@ -179,35 +200,39 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, const mp3g_granule* __
       tprev = t;
     }
   };
-  __shared__ WaveSmem s;
-  const ChunkDesc cd = chunks[blockIdx.x];
-  const int lane = threadIdx.x;
-  const int ch = lane >> 5, k = lane & 31;
-
-  // per-lane constants: matrixing row X_k and window taps of output index k
-  float dct[16], dw[16];
-#pragma unroll
-  for (int j = 0; j < 16; j++) {
-    dct[j] = g_fast.dct[k][j];
-    dw[j] = g_fast.dwin[k][j];
+  __shared__ SharedSmem sh;
+  __shared__ WaveSmem wsm[kWaves];
+  {
+    const int t = threadIdx.x;
+    for (int e = t; e < 4 * 36; e += kLanes * kWaves) (&sh.win[0][0])[e] = (&g_fast.win[0][0])[e];
+    for (int e = t; e < 9 * 18; e += kLanes * kWaves) {
+      const int q = e / 18, m = e % 18;
+      sh.c36p[q][m] = (f2){g_fast.c36[m][q], g_fast.c36[m][9 + q]};
+    }
+    for (int e = t; e < 12 * 8; e += kLanes * kWaves) {
+      const int p = e >> 3, m = e & 7;
+      sh.c12t[p][m] = m < 6 ? g_fast.cos12[m][p] : 0.0f;
+    }
+    for (int e = t; e < 16; e += kLanes * kWaves) (&sh.isr[0][0])[e] = (&g_fast.is_ratio[0][0])[e];
+    for (int e = t; e < 32 * 20; e += kLanes * kWaves) {
+      const int r = e / 20, j = e % 20;
+      sh.dct[r][j] = j < 16 ? g_fast.dct[r][j] : 0.0f;
+      sh.dwin[r][j] = j < 16 ? g_fast.dwin[r][j] : 0.0f;
+    }
   }
+  __syncthreads();  // the only workgroup barrier: the waves are independent from here on
+  const int lane = threadIdx.x & (kLanes - 1);
+  const uint32_t ci = blockIdx.x * kWaves + (threadIdx.x >> 6);
+  if (ci >= n_chunks) return;
+  WaveSmem& s = wsm[threadIdx.x >> 6];
+  const ChunkDesc cd = chunks[ci];
+  const int ch = lane >> 5, k = lane & 31;
   const int ia = k < 16 ? 16 + k : (k == 16 ? 0 : 48 - k);
   const int ib = k < 16 ? 16 - k : k - 16;
-  for (int e = lane; e < 4 * 36; e += kLanes) (&s.win[0][0])[e] = (&g_fast.win[0][0])[e];
-  for (int e = lane; e < 18 * 20; e += kLanes) {
-    const int q = e / 20, m = e % 20;
-    s.c36t[q][m] = m < 18 ? g_fast.c36[m][q] : 0.0f;
-  }
-  for (int e = lane; e < 16; e += kLanes) (&s.isr[0][0])[e] = (&g_fast.is_ratio[0][0])[e];
-  int cur_combo = -1;
-  for (int e = lane; e < 12 * 8; e += kLanes) {
-    const int p = e >> 3, m = e & 7;
-    s.c12t[p][m] = m < 6 ? g_fast.cos12[m][p] : 0.0f;
-  }
 
   uint64_t w;
   int init_in[2];
-  prologue(cd, gran, &w, init_in);
+  prologue(cd, gran, &w, init_in, lane);
   const mp3g_state* sin = state_in ? state_in + cd.stream : nullptr;
 
   // entry state: overlap store in registers, V history as X vectors
@@ -216,15 +241,15 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, const mp3g_granule* __
     const bool from_in = init_in[ch] && sin;
 #pragma unroll
     for (int j = 0; j < 18; j++) st[j] = from_in ? sin->store[ch][k][j] : 0.0f;
-    for (int e = lane; e < 2 * 16 * 32; e += kLanes) {
-      const int c = e >> 9, blk = (e >> 5) & 15, m = e & 31;
+    for (int e = lane; e < 2 * kHist * 32; e += kLanes) {
+      const int c = e / (kHist * 32), blk = (e >> 5) % kHist, m = e & 31;
       const bool in = init_in[c] && sin;
-      s.ring[c][15 - blk][m] = in ? x_from_v(&sin->vvec[c][64 * blk], m) : 0.0f;
+      s.ring[c][kHist - 1 - blk][m] = in ? x_from_v(&sin->vvec[c][64 * blk], m) : 0.0f;
     }
   }
 
   const uint64_t end = cd.out_first + cd.n_out;
-  if (w < end) load_granule(s, gran, coef, w);
+  if (w < end) load_granule(s, gran, coef, w, lane);
   wave_sync();
 
   if constexpr (kStamp) tprev = __builtin_amdgcn_s_memtime();
@@ -236,22 +261,8 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, const mp3g_granule* __
     // lanes of an absent channel mirror channel 0's block layout (no extra divergence)
     const mp3g_channel& C = s.desc.ch[act ? ch : 0];
 
-    // prefetch the next granule (lands during this one)
-    const bool more = g + 1 < end;
-    uint4 p0 = {0, 0, 0, 0}, p1 = p0, p2 = p0, pd = p0;
-    if (more) {
-      const uint4* src = reinterpret_cast<const uint4*>(coef + (g + 1) * MP3G_COEF_PER_GRANULE);
-      p0 = src[lane];
-      p1 = src[lane + 64];
-      if (lane < 16) p2 = src[lane + 128];
-      if (lane < 10) pd = reinterpret_cast<const uint4*>(gran + g + 1)[lane];
-    }
 
     // ---- per-granule front-end parameters: band exponents, band thresholds ----
-    if (combo != cur_combo) {  // (uniform; normally once per chunk)
-      for (int e = lane; e < 576; e += kLanes) s.linfo[e] = g_fast.linfo[combo][e];
-      cur_combo = combo;
-    }
     for (int e = lane; e < 2 * 22 + 2 * 39; e += kLanes) {
       int c, v;
       if (e < 44) {
@@ -282,16 +293,6 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, const mp3g_granule* __
     // ---- front end: requantize (gather through the reorder), lane = (ch, sb = k) ----
     // the lane's 18 line-info words and raw integers are loaded in bulk first
     float x[18];
-    uint32_t info[18];
-    {
-      const uint2* li = reinterpret_cast<const uint2*>(&s.linfo[18 * k]);
-#pragma unroll
-      for (int q = 0; q < 9; q++) {
-        const uint2 v = li[q];
-        info[2 * q] = v.x;
-        info[2 * q + 1] = v.y;
-      }
-    }
     // wave-uniform: every channel of this granule is a long block (no reorder)
     const bool all_long = __builtin_amdgcn_readfirstlane(
         !(s.desc.ch[0].win_switch_flag == 1 && s.desc.ch[0].block_type == 2) &&
@@ -305,19 +306,23 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, const mp3g_granule* __
         xi[2 * q] = (int)(int16_t)(w & 0xffffu);
         xi[2 * q + 1] = (int)(int16_t)(w >> 16);
       }
+      // long band of line j: first band of the subband + band starts among lines 1..j
+      const uint32_t lb = g_fast.lband[combo][k];
       int n4[18];
 #pragma unroll
-      for (int j = 0; j < 18; j++) n4[j] = s.expo[22 * ch + (info[j] & 31)];
+      for (int j = 0; j < 18; j++)
+        n4[j] = s.expo[22 * ch + (int)(lb & 31u) + __builtin_popcount((lb >> 5) & ((2u << j) - 1u))];
 #pragma unroll
       for (int j = 0; j < 18; j++) {
         // (absent-channel lanes compute garbage that nothing reads)
         x[j] = self(18 * k + j < count1, requant_fast(xi[j], n4[j]), (float)xi[j]);
       }
     } else {
+      const uint32_t* li = &g_fast.linfo[combo][18 * k];
 #pragma unroll
       for (int j = 0; j < 18; j++) {
         const int L = 18 * k + j;
-        const uint32_t inf = info[j];
+        const uint32_t inf = li[j];
         const int sfl = inf & 31, sfs = (inf >> 5) & 15, wsrc = (inf >> 9) & 3, wown = (inf >> 11) & 3;
         const int srcr = inf >> 13;
         const bool longlike = !shortblk || (mixed && L < 36);
@@ -355,29 +360,48 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, const mp3g_granule* __
           const float m = (o + sg * x[j]) * inv_sqrt2;
           x[j] = 18 * k + j < msmax ? m : x[j];
         }
-      } else
+      } else {
+        // MS + intensity stereo: rare, branchy and register hungry, so it runs
+        // line-parallel out of LDS -- the ring slots of the current granule are
+        // free until the matrixing and hold exactly 2 x 576 floats.
+        float* X0 = &s.ring[0][kHist][0];
+        float* X1 = &s.ring[1][kHist][0];
 #pragma unroll
-      for (int j = 0; j < 18; j++) {
-        const int L = 18 * k + j;
-        const float o = xl::xor32(x[j]);
-        float l = self(ch, o, x[j]), r = self(ch, x[j], o);
-        const bool msl = ms && L < msmax;
-        const float nl = (l + r) * inv_sqrt2, nr = (l - r) * inv_sqrt2;
-        l = self(msl, nl, l);
-        r = self(msl, nr, r);
-        if (is) {
-          const uint32_t info = s.linfo[L];
+        for (int j = 0; j < 18; j++) (ch ? X1 : X0)[18 * k + j] = x[j];
+        wave_sync();
+#pragma unroll 1
+        for (int L = lane; L < 576; L += kLanes) {
+          float l = X0[L], r = X1[L];
+          if (ms && L < msmax) {
+            const float nl = (l + r) * inv_sqrt2, nr = (l - r) * inv_sqrt2;
+            l = nl;
+            r = nr;
+          }
+          const uint32_t info = g_fast.linfo[combo][L];
           const int sfl = info & 31, sfs = (info >> 5) & 15, wown = (info >> 11) & 3;
           const bool lp = (!short0 ? (sfl < 21) : (mixed0 && sfl < 8)) && sfl >= nl_is;
-          const int pl = seli(lp, (int)C0.scalefac_l[min(sfl, 21)], 7);
-          l = self(pl < 7, l * s.isr[min(pl, 7)][0], l);
-          r = self(pl < 7, r * s.isr[min(pl, 7)][1], r);
+          if (lp) {
+            const int pos = C0.scalefac_l[sfl];
+            if (pos < 7) {
+              l = l * sh.isr[pos][0];
+              r = r * sh.isr[pos][1];
+            }
+          }
           const bool sp = short0 && sfs < 12 && (!mixed0 || sfs >= 3) && sfs >= ns_is;
-          const int ps = seli(sp, (int)C0.scalefac_s[min(sfs, 12)][min(wown, 2)], 7);
-          l = self(ps < 7, l * s.isr[min(ps, 7)][0], l);
-          r = self(ps < 7, r * s.isr[min(ps, 7)][1], r);
+          if (sp) {
+            const int pos = C0.scalefac_s[sfs][wown];
+            if (pos < 7) {
+              l = l * sh.isr[pos][0];
+              r = r * sh.isr[pos][1];
+            }
+          }
+          X0[L] = l;
+          X1[L] = r;
         }
-        x[j] = self(ch, r, l);
+        wave_sync();
+#pragma unroll
+        for (int j = 0; j < 18; j++) x[j] = (ch ? X1 : X0)[18 * k + j];
+        wave_sync();
       }
     }
     {
@@ -407,106 +431,136 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, const mp3g_granule* __
     {
       int bt = C.block_type & 3;
       if (C.win_switch_flag == 1 && C.mixed_block_flag == 1 && k < 2) bt = 0;
-      float r[36];
+      // raw[0..17] + old overlap -> o[], raw[18..35] -> new overlap, written as
+      // each raw value is produced (no 36-entry temporary)
       if (bt == 2) {
+        // raw[pos] = sum over the windows wi with 0 <= pos-6-6wi < 12 of
+        // (sum_m x[wi+3m] cosN12[m][p]) * win[2][p], p = pos-6-6wi (imdct.go:88-94)
 #pragma unroll
-        for (int p = 0; p < 36; p++) r[p] = 0.0f;
-#pragma unroll
-        for (int p = 0; p < 12; p++) {
-          const float4 c0 = *reinterpret_cast<const float4*>(&s.c12t[p][0]);
-          const float2 c1 = *reinterpret_cast<const float2*>(&s.c12t[p][4]);
-          const float cp[6] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y};
-          const float wp = s.win[2][p];
+        for (int pos = 0; pos < 36; pos++) {
+          float raw = 0.0f;
 #pragma unroll
           for (int wi = 0; wi < 3; wi++) {
+            const int p = pos - 6 - 6 * wi;
+            if (p < 0 || p >= 12) continue;
             float sum = 0.0f;
 #pragma unroll
-            for (int m = 0; m < 6; m++) sum += x[wi + 3 * m] * cp[m];
-            r[6 * wi + p + 6] += sum * wp;
+            for (int m = 0; m < 6; m++) sum += x[wi + 3 * m] * sh.c12t[p][m];
+            raw += sum * sh.win[2][p];
           }
+          if (pos < 18) o[pos] = raw + st[pos];
+          else st[pos - 18] = self(act, raw, st[pos - 18]);
         }
       } else {
-        const float* W = s.win[bt];
+        const float* W = sh.win[bt];
 #pragma unroll
         for (int q = 0; q < 9; q++) {
-          float za = 0.0f, zb = 0.0f;
-          const float4* ca = reinterpret_cast<const float4*>(&s.c36t[q][0]);
-          const float4* cb = reinterpret_cast<const float4*>(&s.c36t[9 + q][0]);
+          // (sum_m x[m] cosN36[m][q], sum_m x[m] cosN36[m][18+q]) as one packed chain
+          f2 z = bcast(0.0f);
+          const f2* c = sh.c36p[q];
 #pragma unroll
-          for (int m4 = 0; m4 < 5; m4++) {
-            const float4 a = ca[m4], b = cb[m4];
-            const float av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
-#pragma unroll
-            for (int e = 0; e < 4; e++) {
-              if (4 * m4 + e < 18) {
-                za += x[4 * m4 + e] * av[e];
-                zb += x[4 * m4 + e] * bv[e];
-              }
-            }
-          }
-          r[q] = za * W[q];
-          r[17 - q] = -za * W[17 - q];
-          r[18 + q] = zb * W[18 + q];
-          r[35 - q] = zb * W[35 - q];
+          for (int m = 0; m < 18; m++) z = pfma(bcast(x[m]), c[m], z);
+          o[q] = z.x * W[q] + st[q];
+          o[17 - q] = -z.x * W[17 - q] + st[17 - q];
+          st[q] = self(act, z.y * W[18 + q], st[q]);
+          st[17 - q] = self(act, z.y * W[35 - q], st[17 - q]);
         }
       }
 #pragma unroll
-      for (int j = 0; j < 18; j++) {
-        o[j] = r[j] + st[j];
-        st[j] = self(act, r[18 + j], st[j]);
-        if (j & 1) o[j] = self(k & 1, -o[j], o[j]);
-      }
+      for (int j = 1; j < 18; j += 2) o[j] = self(k & 1, -o[j], o[j]);  // frequency inversion
     }
     wave_sync();  // raw[] fully consumed before eo[] (same LDS) is written
     stamp(3);
-
-    // ---- even/odd fold of S across the subband pair (k, 31-k) ----
-#pragma unroll
-    for (int j = 0; j < 18; j++) {
-      const float oth = xl::xor31(o[j]);
-      if (act) s.a.eo[ch][j][k < 16 ? k : 47 - k] = k < 16 ? o[j] + oth : oth - o[j];
+    // prefetch the next granule: lands during the matrixing and window phases
+    // (issued here, not at the top, so its 16 VGPRs are not live across the
+    // front end and IMDCT)
+    const bool more = g + 1 < end;
+    uint4 p0 = {0, 0, 0, 0}, p1 = p0, p2 = p0, pd = p0;
+    if (more) {
+      const uint4* src = reinterpret_cast<const uint4*>(coef + (g + 1) * MP3G_COEF_PER_GRANULE);
+      p0 = src[lane];
+      p1 = src[lane + 64];
+      if (lane < 16) p2 = src[lane + 128];
+      if (lane < 10) pd = reinterpret_cast<const uint4*>(gran + g + 1)[lane];
     }
-    wave_sync();
-    stamp(4);
 
-    // ---- matrixing: X_k for the 18 slots of this granule ----
+    // ---- matrixing, in two halves of 9 time slots: even/odd fold of S across
+    //      the subband pair (k, 31-k), then X_k of each slot (lane = (ch, m = k)) ----
     bool need_v = true;
     if (!out && g + 1 < cd.out_first) need_v = hdr_nch(gran[g + 1].header) < nch;
-    if (need_v && act) {
-      const float* E = &s.a.eo[ch][0][(k & 1) * 16];
-#pragma unroll 6
-      for (int ss = 0; ss < 18; ss++) {
-        const float4* e4 = reinterpret_cast<const float4*>(E + 32 * ss);
-        float acc = 0.0f;
+    float dct[16];
+    {
+      const float4* d4 = reinterpret_cast<const float4*>(&sh.dct[k][0]);
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-          const float4 e = e4[q];
-          acc += dct[4 * q] * e.x;
-          acc += dct[4 * q + 1] * e.y;
-          acc += dct[4 * q + 2] * e.z;
-          acc += dct[4 * q + 3] * e.w;
-        }
-        s.ring[ch][16 + ss][k] = acc;
+      for (int q = 0; q < 4; q++) {
+        const float4 v = d4[q];
+        dct[4 * q] = v.x;
+        dct[4 * q + 1] = v.y;
+        dct[4 * q + 2] = v.z;
+        dct[4 * q + 3] = v.w;
       }
     }
-    wave_sync();
-    stamp(5);
+#pragma unroll
+    for (int third = 0; third < 3; third++) {
+#pragma unroll
+      for (int pp = 0; pp < 3; pp++) {
+        const int j = 6 * third + 2 * pp;
+        const f2 v = {o[j], o[j + 1]};
+        const f2 oth = {xl::xor31(o[j]), xl::xor31(o[j + 1])};
+        if (act) s.a.eo[ch][pp][k < 16 ? k : 47 - k] = k < 16 ? v + oth : oth - v;
+      }
+      wave_sync();
+      if (need_v && act) {
+        const f2* E = &s.a.eo[ch][0][(k & 1) * 16];
+#pragma unroll
+        for (int pp = 0; pp < 3; pp++) {
+          // X_k of the slot pair (6*third + 2pp, +1)
+          f2 acc = bcast(0.0f);
+#pragma unroll
+          for (int q = 0; q < 16; q++) acc = pfma(bcast(dct[q]), E[32 * pp + q], acc);
+          s.ring[ch][kHist + 6 * third + 2 * pp][k] = acc.x;
+          s.ring[ch][kHist + 6 * third + 2 * pp + 1][k] = acc.y;
+        }
+      }
+      wave_sync();
+      if (third) stamp(3 + third);
+    }
 
     // ---- 16-tap window over the X ring -> s16 PCM ----
     if (out && act) {
-      float acc[18];
+      float dw[16];
+      {
+        const float4* d4 = reinterpret_cast<const float4*>(&sh.dwin[k][0]);
 #pragma unroll
-      for (int ss = 0; ss < 18; ss++) acc[ss] = 0.0f;
+        for (int q = 0; q < 4; q++) {
+          const float4 v = d4[q];
+          dw[4 * q] = v.x;
+          dw[4 * q + 1] = v.y;
+          dw[4 * q + 2] = v.z;
+          dw[4 * q + 3] = v.w;
+        }
+      }
+      // taps (2t, 2t+1) of output ss read X_u[a] and X_{u-1}[b], u = ss - 2t:
+      // one pair P_u per u feeds up to 8 outputs as packed FMAs.  Two passes of
+      // 9 outputs keep the live pairs + accumulators within the register budget.
+      float acc[18];
       const float* R = &s.ring[ch][0][0];
 #pragma unroll
-      for (int u = -15; u < 18; u++) {
-        const float xa = R[(16 + u) * 32 + ia];
-        const float xb = R[(16 + u) * 32 + ib];
+      for (int pass = 0; pass < 2; pass++) {
+        f2 acc2[9];
 #pragma unroll
-        for (int ss = (u > 0 ? u : 0); ss < 18 && ss <= u + 15; ss++) {
-          const int j = ss - u;
-          acc[ss] += dw[j] * ((j & 1) ? xb : xa);
+        for (int i = 0; i < 9; i++) acc2[i] = bcast(0.0f);
+#pragma unroll
+        for (int u = 9 * pass - 14; u < 9 * pass + 9; u++) {
+          const f2 P = {R[(kHist + u) * 32 + ia], R[(kHist + u - 1) * 32 + ib]};
+#pragma unroll
+          for (int t = 0; t < 8; t++) {
+            const int i = u + 2 * t - 9 * pass;
+            if (i >= 0 && i < 9) acc2[i] = pfma((f2){dw[2 * t], dw[2 * t + 1]}, P, acc2[i]);
+          }
         }
+#pragma unroll
+        for (int i = 0; i < 9; i++) acc[9 * pass + i] = acc2[i].x + acc2[i].y;
       }
       uint32_t* dst = reinterpret_cast<uint32_t*>(pcm + g * 1152);
       if (nch == 2) {
@@ -530,8 +584,8 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, const mp3g_granule* __
     stamp(6);
 
     // ---- history shift (channels this granule touched) + next granule in ----
-    for (int e = lane; e < nch * 128; e += kLanes) {
-      const int c = e >> 7, r4 = e & 127;
+    for (int e = lane; e < nch * (kHist * 8); e += kLanes) {
+      const int c = e / (kHist * 8), r4 = e % (kHist * 8);
       reinterpret_cast<float4*>(&s.ring[c][0][0])[r4] = reinterpret_cast<const float4*>(&s.ring[c][18][0])[r4];
     }
     if (more) {
@@ -545,8 +599,8 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, const mp3g_granule* __
     stamp(7);
   }
   if constexpr (kStamp) {
-    if (threadIdx.x == 0)
-      for (int p = 0; p < kPhases; p++) stamps[(size_t)blockIdx.x * kPhases + p] = ph[p];
+    if (lane == 0)
+      for (int p = 0; p < kPhases; p++) stamps[(size_t)ci * kPhases + p] = ph[p];
   }
 
   if (cd.flags & kChunkStateOut) {
@@ -555,7 +609,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, const mp3g_granule* __
     for (int j = 0; j < 18; j++) so->store[ch][k][j] = st[j];
     for (int e = lane; e < 2 * 1024; e += kLanes) {
       const int c = e >> 10, blk = (e >> 6) & 15, i = e & 63;
-      so->vvec[c][64 * blk + i] = v_from_x(s.ring[c][15 - blk], i);
+      so->vvec[c][64 * blk + i] = blk < kHist ? v_from_x(s.ring[c][kHist - 1 - blk], i) : 0.0f;
     }
   }
 }

@@ -39,8 +39,9 @@ hipError_t launch_granule(int variant, const ChunkDesc* d_chunks, uint32_t n_chu
                           hipStream_t stream) {
   if (n_chunks == 0) return hipSuccess;
   if (variant == kVariantFast)
-    hipLaunchKernelGGL(v3::granule_fast_kernel<false>, dim3(n_chunks), dim3(64), 0, stream, d_chunks, d_gran,
-                       d_coef, d_state_in, d_state_out, d_pcm, nullptr);
+    hipLaunchKernelGGL(v3::granule_fast_kernel<false>, dim3((n_chunks + v3::kWaves - 1) / v3::kWaves),
+                       dim3(64 * v3::kWaves), 0, stream, d_chunks, n_chunks, d_gran, d_coef, d_state_in,
+                       d_state_out, d_pcm, nullptr);
   else if (variant == kVariantV1)
     hipLaunchKernelGGL(v1::granule_exact_kernel, dim3(n_chunks), dim3(256), 0, stream, d_chunks,
                        d_gran, d_coef, d_state_in, d_state_out, d_pcm);
@@ -54,8 +55,9 @@ hipError_t launch_fast_stamped(const ChunkDesc* d_chunks, uint32_t n_chunks, con
                                const int16_t* d_coef, const mp3g_state* d_state_in, mp3g_state* d_state_out,
                                int16_t* d_pcm, unsigned long long* d_stamps, hipStream_t stream) {
   if (n_chunks == 0) return hipSuccess;
-  hipLaunchKernelGGL(v3::granule_fast_kernel<true>, dim3(n_chunks), dim3(64), 0, stream, d_chunks, d_gran, d_coef,
-                     d_state_in, d_state_out, d_pcm, d_stamps);
+  hipLaunchKernelGGL(v3::granule_fast_kernel<true>, dim3((n_chunks + v3::kWaves - 1) / v3::kWaves),
+                     dim3(64 * v3::kWaves), 0, stream, d_chunks, n_chunks, d_gran, d_coef, d_state_in, d_state_out,
+                     d_pcm, d_stamps);
   return hipGetLastError();
 }
 
