@@ -230,9 +230,15 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
   const int ia = k < 16 ? 16 + k : (k == 16 ? 0 : 48 - k);
   const int ib = k < 16 ? 16 - k : k - 16;
 
-  uint64_t w;
+  uint64_t w64;
   int init_in[2];
-  prologue(cd, gran, &w, init_in, lane);
+  prologue(cd, gran, &w64, init_in, lane);
+  // loop state as wave-uniform 32-bit scalars (plans are limited to < 2^32
+  // granules): keeps it in SGPRs, so per-granule header reads are scalar loads
+  // (lgkmcnt) that never wait behind the prefetch loads or PCM stores (vmcnt)
+  const uint32_t w = __builtin_amdgcn_readfirstlane((uint32_t)w64);
+  const uint32_t out_first = __builtin_amdgcn_readfirstlane((uint32_t)cd.out_first);
+  const uint32_t end = __builtin_amdgcn_readfirstlane((uint32_t)(cd.out_first + cd.n_out));
   const mp3g_state* sin = state_in ? state_in + cd.stream : nullptr;
 
   // entry state: overlap store in registers, V history as X vectors
@@ -248,13 +254,15 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     }
   }
 
-  const uint64_t end = cd.out_first + cd.n_out;
   if (w < end) load_granule(s, gran, coef, w, lane);
   wave_sync();
 
   if constexpr (kStamp) tprev = __builtin_amdgcn_s_memtime();
-  for (uint64_t g = w; g < end; g++) {
-    const bool out = g >= cd.out_first;
+  for (uint32_t g = w; g < end; g++) {
+    const bool out = g >= out_first;
+    // does a replayed granule's V feed anything? (see v2 / DESIGN.md halo)
+    bool need_v = true;
+    if (!out && g + 1 < out_first) need_v = hdr_nch(gran[g + 1].header) < hdr_nch(s.desc.header);
     const uint32_t h = s.desc.header;
     const int nch = hdr_nch(h), combo = hdr_combo(h);
     const bool act = ch < nch;
@@ -477,7 +485,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     const bool more = g + 1 < end;
     uint4 p0 = {0, 0, 0, 0}, p1 = p0, p2 = p0, pd = p0;
     if (more) {
-      const uint4* src = reinterpret_cast<const uint4*>(coef + (g + 1) * MP3G_COEF_PER_GRANULE);
+      const uint4* src = reinterpret_cast<const uint4*>(coef + (size_t)(g + 1) * MP3G_COEF_PER_GRANULE);
       p0 = src[lane];
       p1 = src[lane + 64];
       if (lane < 16) p2 = src[lane + 128];
@@ -486,8 +494,6 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
 
     // ---- matrixing, in two halves of 9 time slots: even/odd fold of S across
     //      the subband pair (k, 31-k), then X_k of each slot (lane = (ch, m = k)) ----
-    bool need_v = true;
-    if (!out && g + 1 < cd.out_first) need_v = hdr_nch(gran[g + 1].header) < nch;
     float dct[16];
     {
       const float4* d4 = reinterpret_cast<const float4*>(&sh.dct[k][0]);
@@ -562,7 +568,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
 #pragma unroll
         for (int i = 0; i < 9; i++) acc[9 * pass + i] = acc2[i].x + acc2[i].y;
       }
-      uint32_t* dst = reinterpret_cast<uint32_t*>(pcm + g * 1152);
+      uint32_t* dst = reinterpret_cast<uint32_t*>(pcm + (size_t)g * 1152);
       if (nch == 2) {
 #pragma unroll
         for (int q = 0; q < 9; q++) {
