@@ -75,7 +75,7 @@ def profiled_traffic(cfg, kernel):
     files = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_{cfg}.json")))
     for f in reversed(files):
         d = json.load(open(f))
-        if d.get("kernel") == kernel and d.get("hbm_bytes_per_launch_corrected"):
+        if kernel in d.get("kernel", "") and d.get("hbm_bytes_per_launch_corrected"):
             return d["hbm_bytes_per_launch_corrected"], os.path.relpath(f, REPO)
     return None, None
 
