@@ -65,17 +65,21 @@ struct __align__(16) SharedSmem {
   f2 c36p[9][18];      // distinct cosN36 columns as pairs (col q, col 18+q): [q][m]
   float c12t[12][8];   // cosN12 transposed [p][m] (rows padded to 2 x float4)
   float isr[8][2];
-  float dct[32][20];   // FastTables::dct rows (padded: conflict-free b128 row reads)
-  float dwin[32][20];  // FastTables::dwin rows
+  float dct[32][16];   // FastTables::dct rows (one row per lane, read once per granule)
+  float dwin[32][16];  // FastTables::dwin rows, pre-scaled by 32767
 };
-// per-wave working set: 11.4 KB -> 3 workgroups (12 waves) per CU
+// per-wave working set ~11.9 KB.  The workgroup (4 waves + shared tables) must
+// stay <= 42 x 1280 B (gfx950 LDS allocation granule) for 3 workgroups
+// (12 waves) per CU.
 struct __align__(16) WaveSmem {
   union {
     int16_t raw[2][576];  // Huffman integers of the current granule
     f2 eo[2][3][32];      // folded matrixing input of 6 slots [ch][slot pair][k]: even k<16, odd 16+k
+    int16_t pcm[576 * 2]; // s16 stereo output staged for 16-B stores
   } a;
   float ring[2][kRing][32];
-  int expo[2 * 22 + 2 * 39];  // requantization exponents n4: long bands [ch][sfb], short [ch][sfb][win]
+  // requantization exponents n4 of the long bands [ch][sfb] and short bands [ch][sfb][win]
+  int expo[2 * 22 + 2 * 39];
   mp3g_granule desc;
 };
 
@@ -161,14 +165,13 @@ __device__ __forceinline__ int seli(bool c, int a, int b) {
   return (a & m) | (b & ~m);
 }
 
-// |x|^(4/3) * 2^(n4/4) = ldexp(|x| * 2^(log2|x| / 3 + (n4 & 3) / 4), n4 >> 2), signed:
+// sign(x) |x|^(4/3) 2^(n4/4) = ldexp(2^(4/3 log2|x| + (n4 & 3)/4), n4 >> 2), signed:
 // two transcendental VALU ops instead of the float64 table gather of the
 // reference (frame.go:148-155); relative error ~1e-6 (x = 0 -> exactly 0).
 __device__ __forceinline__ float requant_fast(int xi, int n4) {
-  const float ax = (float)abs(xi);
-  const float t = __builtin_amdgcn_logf(ax) * (1.0f / 3.0f) + 0.25f * (float)(n4 & 3);
-  const float mag = ldexpf(ax * __builtin_amdgcn_exp2f(t), n4 >> 2);
-  return xi < 0 ? -mag : mag;
+  const float xf = (float)xi;
+  const float t = __builtin_amdgcn_logf(fabsf(xf)) * (4.0f / 3.0f) + 0.25f * (float)(n4 & 3);
+  return copysignf(ldexpf(__builtin_amdgcn_exp2f(t), n4 >> 2), xf);
 }
 
 // X of a V block: X[m] = V[m-16] (m >= 16), -V[48-m] (m < 16).
@@ -214,10 +217,9 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       sh.c12t[p][m] = m < 6 ? g_fast.cos12[m][p] : 0.0f;
     }
     for (int e = t; e < 16; e += kLanes * kWaves) (&sh.isr[0][0])[e] = (&g_fast.is_ratio[0][0])[e];
-    for (int e = t; e < 32 * 20; e += kLanes * kWaves) {
-      const int r = e / 20, j = e % 20;
-      sh.dct[r][j] = j < 16 ? g_fast.dct[r][j] : 0.0f;
-      sh.dwin[r][j] = j < 16 ? g_fast.dwin[r][j] : 0.0f;
+    for (int e = t; e < 32 * 16; e += kLanes * kWaves) {
+      (&sh.dct[0][0])[e] = (&g_fast.dct[0][0])[e];
+      (&sh.dwin[0][0])[e] = (&g_fast.dwin[0][0])[e] * 32767.0f;
     }
   }
   __syncthreads();  // the only workgroup barrier: the waves are independent from here on
@@ -244,12 +246,14 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
   // entry state: overlap store in registers, V history as X vectors
   float st[18];
   {
-    const bool from_in = init_in[ch] && sin;
+    // (no dynamic indexing of init_in[]: a private array would be promoted to LDS)
+    const bool in0 = init_in[0] && sin, in1 = init_in[1] && sin;
+    const bool from_in = ch ? in1 : in0;
 #pragma unroll
     for (int j = 0; j < 18; j++) st[j] = from_in ? sin->store[ch][k][j] : 0.0f;
     for (int e = lane; e < 2 * kHist * 32; e += kLanes) {
       const int c = e / (kHist * 32), blk = (e >> 5) % kHist, m = e & 31;
-      const bool in = init_in[c] && sin;
+      const bool in = c ? in1 : in0;
       s.ring[c][kHist - 1 - blk][m] = in ? x_from_v(&sin->vvec[c][64 * blk], m) : 0.0f;
     }
   }
@@ -316,15 +320,16 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       }
       // long band of line j: first band of the subband + band starts among lines 1..j
       const uint32_t lb = g_fast.lband[combo][k];
-      int n4[18];
+      int ex[18];
 #pragma unroll
       for (int j = 0; j < 18; j++)
-        n4[j] = s.expo[22 * ch + (int)(lb & 31u) + __builtin_popcount((lb >> 5) & ((2u << j) - 1u))];
+        ex[j] = s.expo[22 * ch + (int)(lb & 31u) + __builtin_popcount((lb >> 5) & ((2u << j) - 1u))];
+      // Lines >= count1 hold zeros (the bitstream parse's guarantee,
+      // maindata/huffman.go:130-134; mp3g_validate checks it), and requantizing
+      // 0 gives 0, so long blocks need no per-line count1 test here.
+      // (absent-channel lanes compute garbage that nothing reads)
 #pragma unroll
-      for (int j = 0; j < 18; j++) {
-        // (absent-channel lanes compute garbage that nothing reads)
-        x[j] = self(18 * k + j < count1, requant_fast(xi[j], n4[j]), (float)xi[j]);
-      }
+      for (int j = 0; j < 18; j++) x[j] = requant_fast(xi[j], ex[j]);
     } else {
       const uint32_t* li = &g_fast.linfo[combo][18 * k];
 #pragma unroll
@@ -341,8 +346,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
         const int eidx = seli(longlike, 22 * ch + sfl, 44 + 39 * ch + 3 * sfs + win);
         const bool process = longlike ? (shortblk || L < count1) : started;
         const int xi = s.a.raw[ch][src];
-        const int n4 = s.expo[eidx];
-        x[j] = self(process, requant_fast(xi, n4), (float)xi);
+        x[j] = self(process, requant_fast(xi, s.expo[eidx]), (float)xi);
       }
     }
     stamp(1);
@@ -568,25 +572,25 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
 #pragma unroll
         for (int i = 0; i < 9; i++) acc[9 * pass + i] = acc2[i].x + acc2[i].y;
       }
-      uint32_t* dst = reinterpret_cast<uint32_t*>(pcm + (size_t)g * 1152);
-      if (nch == 2) {
+      // s16 into the LDS staging area (raw/eo are dead until the next granule
+      // is written in), then 16-B coalesced stores
+      int16_t* P = s.a.pcm;
 #pragma unroll
-        for (int q = 0; q < 9; q++) {
-          const int a = pcm_sample(acc[2 * q]), b = pcm_sample(acc[2 * q + 1]);
-          const int got = xl::xor32i(ch ? a : b);
-          // lane (0,k) stores slot 2q, lane (1,k) slot 2q+1: (L, R) = low, high half
-          const int L = ch ? got : a, Rr = ch ? b : got;
-          dst[32 * (2 * q + ch) + k] = (uint32_t)(L & 0xffff) | ((uint32_t)Rr << 16);
-        }
-      } else {
-#pragma unroll
-        for (int ss = 0; ss < 18; ss++) {
-          const uint32_t v = (uint32_t)pcm_sample(acc[ss]) & 0xffffu;
-          dst[32 * ss + k] = v | (v << 16);
-        }
+      for (int ss = 0; ss < 18; ss++) {
+        const int16_t v = (int16_t)(int)__builtin_amdgcn_fmed3f(acc[ss], -32767.0f, 32767.0f);
+        P[2 * (32 * ss + k) + ch] = v;
+        if (nch == 1) P[2 * (32 * ss + k) + 1] = v;  // mono: both slots (frame.go:671-678)
       }
     }
-    wave_sync();  // ring reads done
+    if (out) {
+      wave_sync();
+      const uint4* src = reinterpret_cast<const uint4*>(s.a.pcm);
+      uint4* dst = reinterpret_cast<uint4*>(pcm + (size_t)g * 1152);
+      dst[lane] = src[lane];
+      dst[lane + 64] = src[lane + 64];
+      if (lane < 16) dst[lane + 128] = src[lane + 128];
+    }
+    wave_sync();  // ring reads done, staging area free
     stamp(6);
 
     // ---- history shift (channels this granule touched) + next granule in ----
