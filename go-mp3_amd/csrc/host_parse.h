@@ -1,0 +1,78 @@
+// host_parse.h -- product host-side bitstream parse of an MP3 byte stream into
+// the granule boundary input of the GPU path.
+//
+// This is the part of go-mp3's per-frame pipeline that stays on the CPU:
+// source/tag handling (source.go:42-122), frame header + sync search
+// (frameheader.go:279-328), side info (sideinfo.go:33-156), bit reservoir
+// (maindata.go:290-323), scale factors (maindata.go:119-288) and Huffman
+// decoding (maindata/huffman.go:27-138, huffman/huffman.go:348-419).  The
+// semantics (including the reference's quirks: reservoir underflow, zero
+// reads past the end of the main data, count1 back-off) are the reference's;
+// the implementation is table driven: Huffman codewords are decoded with
+// two-level lookup tables built from ISO 11172-3 Table B.7 instead of a
+// bit-serial tree walk, and the output is written straight into
+// mp3g_granule descriptors + int16 coefficients.
+#pragma once
+#include <cstdint>
+#include <vector>
+
+#include "../../include/mp3g.h"
+
+namespace mp3g {
+namespace host {
+
+// Error classes the reference's decode.go distinguishes.
+enum class St { kOk = 0, kEof = 1, kErr = 2, kPanic = 3 };
+
+// source.go over an in-memory bytes.Reader (seekable = implements io.Seeker).
+struct Source {
+  const uint8_t* data = nullptr;
+  int64_t len = 0;
+  int64_t rpos = 0;  // reader position
+  bool seekable = true;
+  uint8_t unread[16];
+  int n_unread = 0;
+  int64_t pos = 0;  // source.pos
+
+  int64_t read_full(uint8_t* buf, int64_t n, bool* short_read);
+  void unread_bytes(const uint8_t* b, int n);
+  bool seek(int64_t off, int whence, int64_t* res);
+  St skip_tags();
+};
+
+// One parsed frame: its header, start offset and the boundary input of its
+// granules (2 for MPEG-1, 1 for MPEG-2 LSF).
+struct ParsedFrame {
+  uint32_t header = 0;
+  int64_t start = 0;
+  int n_granules = 0;
+  mp3g_granule gran[2];
+  int16_t coef[2][MP3G_COEF_PER_GRANULE];
+};
+
+// Carries the bit reservoir between frames (frame.Read's `prev`).
+class FrameParser {
+ public:
+  // Parses the next frame at the source's position (frame.go:67-115).
+  // prev_frame = false reproduces frame.Read(source, pos, nil) -- after a
+  // seek the reservoir is empty.
+  St next(Source& src, ParsedFrame* out);
+  void reset() { have_prev_ = false; prev_md_.clear(); }
+
+ private:
+  bool have_prev_ = false;
+  std::vector<uint8_t> prev_md_;  // previous frame's main-data bytes
+  std::vector<uint8_t> md_;       // scratch
+};
+
+// frameheader.Read: sync search from the source position.
+St read_header(Source& s, int64_t* pos_io, uint32_t* out);
+
+// frameheader accessors used by the decoder
+int header_bytes_per_frame(uint32_t h);
+int header_frame_size(uint32_t h);
+int header_sample_rate(uint32_t h);
+int header_granules(uint32_t h);
+
+}  // namespace host
+}  // namespace mp3g

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "../../include/mp3g.h"
+#include "abi_util.h"
 #include "dsp_tables.h"
 #include "kernels.h"
 
@@ -84,6 +85,8 @@ int ensure_device(int dev) {
 }
 
 }  // namespace
+
+int mp3g::abi_fail(int status, const char* what) { return fail(status, what); }
 
 struct mp3g_plan {
   int device = 0;

@@ -14,7 +14,8 @@ import numpy as np
 
 __all__ = ["CHANNEL_DTYPE", "GRANULE_DTYPE", "STREAM_DTYPE", "STATE_DTYPE", "MODE_EXACT",
            "MODE_FAST", "FLAG_CHECKED", "FLAG_KERNEL_V1", "STATE_IN", "STATE_OUT", "Mp3gError", "lib", "lib_path",
-           "decode_host", "validate", "Plan", "device_count", "streams_for"]
+           "decode_host", "validate", "Plan", "device_count", "streams_for", "parse_stream",
+           "parse_streams", "Decoder"]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 
@@ -70,6 +71,25 @@ def lib():
         L.mp3g_plan_execute.argtypes = [vp, vp, vp, vp, vp, vp, vp]
         L.mp3g_decode_host.argtypes = [C.c_int, vp, vp, u64, vp, u32, vp, vp, vp, u32]
         L.mp3g_plan_debug_phases.argtypes = [vp, vp, vp, vp, C.POINTER(u64), vp]
+        i64, sz = C.c_int64, C.c_size_t
+        L.mp3g_parse_stream.argtypes = [vp, sz, C.POINTER(vp), C.POINTER(vp), C.POINTER(u64),
+                                        C.POINTER(C.c_int)]
+        L.mp3g_parse_streams.argtypes = [u32, vp, vp, C.c_int, C.POINTER(vp), C.POINTER(vp),
+                                         C.POINTER(u64), vp, vp]
+        L.mp3g_free.argtypes = [vp]
+        L.mp3g_decoder_new.argtypes = [vp, sz, C.c_int, C.c_int, u32, C.POINTER(vp)]
+        L.mp3g_decoder_free.argtypes = [vp]
+        L.mp3g_decoder_read.argtypes = [vp, vp, sz, C.POINTER(sz)]
+        L.mp3g_decoder_seek.argtypes = [vp, i64, C.c_int, C.POINTER(i64)]
+        L.mp3g_decoder_info.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(i64), C.POINTER(i64),
+                                        C.POINTER(i64)]
+        for fn in ("duration_ns", "position_ns", "remaining_ns", "sample_position", "sample_count"):
+            getattr(L, "mp3g_decoder_" + fn).argtypes = [vp]
+            getattr(L, "mp3g_decoder_" + fn).restype = i64
+        L.mp3g_decoder_progress.argtypes = [vp]
+        L.mp3g_decoder_progress.restype = C.c_double
+        for fn in ("seek_to_sample", "seek_to_time_ns", "skip_ns"):
+            getattr(L, "mp3g_decoder_" + fn).argtypes = [vp, i64]
         _lib = L
     return _lib
 
@@ -129,6 +149,104 @@ def decode_host(granules, coeffs, streams=None, state_in=None, state_out=None, m
     _check(lib().mp3g_decode_host(device, _ptr(granules), _ptr(coeffs), n, _ptr(streams),
                                   len(streams), _ptr(state_in), _ptr(state_out), _ptr(pcm), mode))
     return pcm, state_out
+
+
+def _take(ptr, n, dtype, shape):
+    out = np.frombuffer(C.string_at(ptr, n * np.dtype(dtype).itemsize * int(np.prod(shape[1:]))),
+                        dtype=dtype).reshape(shape).copy() if n else np.zeros(shape, dtype)
+    lib().mp3g_free(ptr)
+    return out
+
+
+def parse_stream(data: bytes):
+    """Host bitstream parse (mp3g_parse_stream): (granules, coeffs [n,2,576], end_status)."""
+    buf = np.frombuffer(data, dtype=np.uint8) if len(data) else np.zeros(1, np.uint8)
+    g, c, n, st = C.c_void_p(), C.c_void_p(), C.c_uint64(), C.c_int()
+    _check(lib().mp3g_parse_stream(_ptr(buf), len(data), C.byref(g), C.byref(c), C.byref(n), C.byref(st)))
+    k = n.value
+    return (_take(g, k, GRANULE_DTYPE, (k,)), _take(c, k, np.int16, (k, 2, 576)), st.value)
+
+
+def parse_streams(datas, n_threads=0):
+    """Many streams in parallel: (granules, coeffs, streams[STREAM_DTYPE], end_status[])."""
+    bufs = [np.frombuffer(d, dtype=np.uint8) if len(d) else np.zeros(1, np.uint8) for d in datas]
+    ptrs = (C.c_void_p * max(1, len(bufs)))(*[b.ctypes.data for b in bufs])
+    lens = (C.c_size_t * max(1, len(bufs)))(*[len(d) for d in datas])
+    streams = np.zeros(len(datas), STREAM_DTYPE)
+    status = np.zeros(max(1, len(datas)), np.int32)
+    g, c, n = C.c_void_p(), C.c_void_p(), C.c_uint64()
+    _check(lib().mp3g_parse_streams(len(datas), ptrs, lens, n_threads, C.byref(g), C.byref(c), C.byref(n),
+                                    _ptr(streams), _ptr(status)))
+    k = n.value
+    return (_take(g, k, GRANULE_DTYPE, (k,)), _take(c, k, np.int16, (k, 2, 576)), streams,
+            status[:len(datas)])
+
+
+class Decoder:
+    """mp3.Decoder (reference decode.go:27-388) backed by the GPU path.
+
+    read(n) -> (status, bytes): status 0 with >= 1 byte, 7 (EOF) or an error
+    status, like Decoder.Read.  seek(off, whence) -> (status, newpos)."""
+
+    def __init__(self, data: bytes, seekable=True, mode=MODE_EXACT, device=0):
+        buf = np.frombuffer(data, dtype=np.uint8) if len(data) else np.zeros(1, np.uint8)
+        self._h = C.c_void_p()
+        _check(lib().mp3g_decoder_new(_ptr(buf), len(data), int(seekable), device, mode, C.byref(self._h)))
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            lib().mp3g_decoder_free(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def read(self, n):
+        out = np.zeros(max(n, 1), np.uint8)
+        k = C.c_size_t()
+        st = lib().mp3g_decoder_read(self._h, _ptr(out), n, C.byref(k))
+        return st, out[:k.value].tobytes()
+
+    def read_all(self):
+        chunks = []
+        while True:
+            st, b = self.read(1 << 16)
+            if st != 0:
+                return st, b"".join(chunks)
+            chunks.append(b)
+
+    def seek(self, off, whence=0):
+        np_ = C.c_int64()
+        st = lib().mp3g_decoder_seek(self._h, off, whence, C.byref(np_))
+        return st, np_.value
+
+    def _info(self):
+        sr, ln, bpf, pos = C.c_int(), C.c_int64(), C.c_int64(), C.c_int64()
+        _check(lib().mp3g_decoder_info(self._h, C.byref(sr), C.byref(ln), C.byref(bpf), C.byref(pos)))
+        return sr.value, ln.value, bpf.value, pos.value
+
+    sample_rate = property(lambda self: self._info()[0])
+    length = property(lambda self: self._info()[1])
+    bytes_per_frame = property(lambda self: self._info()[2])
+    pos = property(lambda self: self._info()[3])
+    duration_ns = property(lambda self: lib().mp3g_decoder_duration_ns(self._h))
+    position_ns = property(lambda self: lib().mp3g_decoder_position_ns(self._h))
+    remaining_ns = property(lambda self: lib().mp3g_decoder_remaining_ns(self._h))
+    progress = property(lambda self: lib().mp3g_decoder_progress(self._h))
+    sample_position = property(lambda self: lib().mp3g_decoder_sample_position(self._h))
+    sample_count = property(lambda self: lib().mp3g_decoder_sample_count(self._h))
+
+    def seek_to_sample(self, s):
+        return lib().mp3g_decoder_seek_to_sample(self._h, s)
+
+    def seek_to_time_ns(self, t):
+        return lib().mp3g_decoder_seek_to_time_ns(self._h, t)
+
+    def skip_ns(self, d):
+        return lib().mp3g_decoder_skip_ns(self._h, d)
 
 
 class Plan:

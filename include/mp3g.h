@@ -165,6 +165,51 @@ int mp3g_decode_host(int device, const mp3g_granule* granules, const int16_t* co
                      const mp3g_state* state_in, mp3g_state* state_out, int16_t* pcm,
                      uint32_t mode);
 
+/* ---- host bitstream parse (CPU only) -----------------
+ * The part of go-mp3's frame.Read that feeds Decode: tags (source.go:42-83),
+ * sync search + header (frameheader.go:279-328), side info (sideinfo.go),
+ * bit reservoir (maindata.go:290-323), scale factors and Huffman decoding
+ * (maindata.go:119-288, maindata/huffman.go:27-138).  Output buffers are
+ * allocated by the library (free with mp3g_free).  *end_status is MP3G_EOF
+ * when the stream ended the way decode.go maps to io.EOF, MP3G_ERR_PARSE for
+ * any other frame.Read error, MP3G_ERR_UNSUPPORTED where the reference would
+ * panic; the granules of every frame before that point are returned. */
+int mp3g_parse_stream(const uint8_t* data, size_t len, mp3g_granule** granules, int16_t** coeffs,
+                      uint64_t* n_granules, int* end_status);
+/* Many independent streams on n_threads host threads (0 = all cores); the
+ * stream table describes where each stream's granules landed. */
+int mp3g_parse_streams(uint32_t n_streams, const uint8_t* const* datas, const size_t* lens, int n_threads,
+                       mp3g_granule** granules, int16_t** coeffs, uint64_t* n_granules, mp3g_stream* streams,
+                       int* end_status);
+void mp3g_free(void* p);
+
+/* ---- decoder: mp3.NewDecoder / io.Reader / io.Seeker (decode.go:27-388) ----
+ * Parses on the host with read-ahead and decodes batches of frames on
+ * `device` (mode = MP3G_MODE_EXACT | MP3G_MODE_FAST).  `data` is copied.
+ * seekable = 0 models a reader that is not an io.Seeker (Length = -1).
+ * Read returns MP3G_OK with *n >= 1, MP3G_EOF, or the error of the frame
+ * that failed (after all PCM before it was delivered) -- like Decoder.Read. */
+typedef struct mp3g_decoder mp3g_decoder;
+int mp3g_decoder_new(const uint8_t* data, size_t len, int seekable, int device, uint32_t mode,
+                     mp3g_decoder** out);
+void mp3g_decoder_free(mp3g_decoder* dec);
+int mp3g_decoder_read(mp3g_decoder* dec, uint8_t* buf, size_t cap, size_t* n);
+/* whence: 0 = io.SeekStart, 1 = io.SeekCurrent, 2 = io.SeekEnd */
+int mp3g_decoder_seek(mp3g_decoder* dec, int64_t offset, int whence, int64_t* newpos);
+/* SampleRate, Length (-1 if unknown), BytesPerFrame, current position (bytes) */
+int mp3g_decoder_info(const mp3g_decoder* dec, int* sample_rate, int64_t* length, int64_t* bytes_per_frame,
+                      int64_t* position);
+/* time API; durations are time.Duration nanoseconds */
+int64_t mp3g_decoder_duration_ns(const mp3g_decoder* dec);
+int64_t mp3g_decoder_position_ns(const mp3g_decoder* dec);
+int64_t mp3g_decoder_remaining_ns(const mp3g_decoder* dec);
+double mp3g_decoder_progress(const mp3g_decoder* dec);
+int64_t mp3g_decoder_sample_position(const mp3g_decoder* dec);
+int64_t mp3g_decoder_sample_count(const mp3g_decoder* dec);
+int mp3g_decoder_seek_to_sample(mp3g_decoder* dec, int64_t sample);
+int mp3g_decoder_seek_to_time_ns(mp3g_decoder* dec, int64_t t_ns);
+int mp3g_decoder_skip_ns(mp3g_decoder* dec, int64_t delta_ns);
+
 /* ---- diagnostics (not part of the decode contract) -----------------------
  * Runs a FAST-mode plan once through the s_memtime-instrumented build of the
  * fast kernel and returns, per kernel phase, the shader cycles summed over

@@ -1,0 +1,142 @@
+"""The decoder API of the product (mp3g_decoder_*: mp3.NewDecoder / Read /
+Seek / time API, reference decode.go:27-388) on the GPU vs the oracle's
+Decoder, operation by operation.
+
+Exact mode: every Read returns the same status and the same bytes as the
+oracle, every Seek the same status and position (bit-exact PCM across the
+read-ahead batch boundaries, seeks, errors and EOF).  Fast mode: the same
+byte counts / statuses / positions, PCM within +-1 LSB.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from test_oracle_kats import ape_tag, id3v1, minimal_frame
+from test_parse_cpu import mutations
+
+pytestmark = pytest.mark.gpu
+
+# oracle status -> product status (Read / Seek)
+ST = {oracle.ORC_OK: 0, oracle.ORC_EOF: 7, oracle.ORC_ERR: 6, oracle.ORC_ERR_PANIC: 8}
+
+
+def both(gpu, data, seekable=True, mode=0):
+    return gpu.Decoder(data, seekable=seekable, mode=mode), oracle.Decoder(data, seekable=seekable)
+
+
+def read_all_both(d, o):
+    st, b = d.read_all()
+    st2, b2 = o.read_all()
+    assert st == ST[st2], (st, st2)
+    return b, b2
+
+
+@pytest.mark.parametrize("name", ["classic_lame.mp3", "mpeg2.mp3"])
+def test_read_all_exact(gpu, sample_files, golden, name):
+    import hashlib
+    d, o = both(gpu, sample_files[name])
+    assert (d.sample_rate, d.length, d.bytes_per_frame) == (o.sample_rate, o.length, o.bytes_per_frame)
+    assert d.duration_ns == o.duration_ns
+    b, b2 = read_all_both(d, o)
+    assert b == b2
+    assert hashlib.sha256(b).hexdigest() == golden["files"][name]["pcm_sha256"]
+
+
+@pytest.mark.parametrize("name", ["classic_lame.mp3", "mpeg2.mp3"])
+def test_read_all_fast(gpu, sample_files, name):
+    d, o = both(gpu, sample_files[name], mode=gpu.MODE_FAST)
+    b, b2 = read_all_both(d, o)
+    assert len(b) == len(b2)
+    diff = np.abs(np.frombuffer(b, np.int16).astype(np.int32) - np.frombuffer(b2, np.int16))
+    assert diff.max() <= 1 and (diff > 0).mean() < 0.01
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_random_seek_read_sequence(gpu, sample_files, mode):
+    rng = np.random.default_rng(7 + mode)
+    for name in ("classic_lame.mp3", "mpeg2.mp3"):
+        d, o = both(gpu, sample_files[name], mode=mode)
+        L = o.length
+        for step in range(120):
+            op = rng.integers(0, 6)
+            if op < 3:
+                n = int(rng.choice([1, 3, 100, 4096, 4608, 20000, 300000]))
+                st, b = d.read(n)
+                st2, b2 = o.read(n)
+                assert st == ST[st2] and len(b) == len(b2), (name, step, st, st2)
+                if mode == 0:
+                    assert b == b2, (name, step)
+                elif b:
+                    diff = np.abs(np.frombuffer(b[:len(b) // 2 * 2], np.int16).astype(np.int32)
+                                  - np.frombuffer(b2[:len(b2) // 2 * 2], np.int16))
+                    assert diff.max(initial=0) <= 1
+            elif op == 3:
+                whence = int(rng.integers(0, 3))
+                off = int(rng.integers(-L // 4, L + 10000))
+                if whence == 1:
+                    off = int(rng.integers(-L // 2, L // 2))
+                if whence == 2:
+                    off = -int(rng.integers(0, L))
+                r, r2 = d.seek(off, whence), o.seek(off, whence)
+                assert (r[0], r[1]) == (ST[r2[0]], r2[1]), (name, step, off, whence, r, r2)
+            elif op == 4:
+                t = int(rng.integers(-10**9, o.duration_ns + 10**9))
+                assert d.seek_to_time_ns(t) == ST[o.seek_to_time_ns(t)]
+            else:
+                s = int(rng.integers(-100, L // 4 + 100))
+                assert d.seek_to_sample(s) == ST[o.seek_to_sample(s)]
+            assert d.pos == o.pos and d.position_ns == o.position_ns, (name, step)
+
+
+def test_time_api_values(gpu, sample_files):
+    d, o = both(gpu, sample_files["mpeg2.mp3"])
+    assert d.seek_to_time_ns(30_000_000_000) == 0 and o.seek_to_time_ns(30_000_000_000) == 0
+    assert d.position_ns == o.position_ns and d.position_ns // 1_000_000 == 30_000
+    assert d.sample_position == d.pos // 4 and d.sample_count == d.length // 4
+    assert d.remaining_ns == d.duration_ns - d.position_ns
+    assert abs(d.progress - d.pos / d.length) < 1e-12
+    assert d.skip_ns(-5_000_000_000) == 0 and d.position_ns // 1_000_000 == 25_000
+    st, b = d.read(4096)
+    st2, b2 = o.read(4096) if o.seek_to_time_ns(25_000_000_000) == 0 else (None, None)
+    assert st == 0 and b == b2
+
+
+def test_non_seekable(gpu, sample_files):
+    d, o = both(gpu, sample_files["classic_lame.mp3"], seekable=False)
+    assert d.length == -1 and d.duration_ns == -1 and d.progress == -1 and d.sample_count == -1
+    b, b2 = read_all_both(d, o)
+    assert b == b2 and len(b) == 385 * 4608
+    assert d.seek_to_sample(10) != 0  # seek not supported
+
+
+@pytest.mark.parametrize("trailer", ["ape", "id3v1", "ape+id3v1", "garbage"])
+def test_trailing_tags(gpu, trailer):
+    tail = {"ape": ape_tag(), "id3v1": id3v1(), "ape+id3v1": ape_tag() + id3v1(),
+            "garbage": bytes(np.random.default_rng(1).integers(0, 255, 100 * 1024, dtype=np.uint8) & 0x7F)}[trailer]
+    data = minimal_frame() * 10 + tail
+    d, o = both(gpu, data)
+    b, b2 = read_all_both(d, o)
+    assert b == b2 and len(b) == 10 * 4608 and not any(b)
+
+
+def test_corrupted_streams_statuses(gpu, sample_files):
+    """Errors mid-stream: PCM before the failing frame, then the error, then
+    decoding resumes from the source position with empty reservoir / zero state."""
+    rng = np.random.default_rng(99)
+    checked = 0
+    for data in mutations(sample_files["classic_lame.mp3"][:80000], rng, 40):
+        try:
+            o = oracle.Decoder(data)
+        except IOError:
+            with pytest.raises(gpu.Mp3gError):
+                gpu.Decoder(data)
+            continue
+        d = gpu.Decoder(data)
+        for _ in range(400):  # read until EOF, through any number of errors
+            st, b = d.read(50000)
+            st2, b2 = o.read(50000)
+            assert st == ST[st2] and b == b2
+            if st2 == oracle.ORC_EOF:
+                break
+        checked += 1
+    assert checked > 10
