@@ -152,8 +152,13 @@ def decode_host(granules, coeffs, streams=None, state_in=None, state_out=None, m
 
 
 def _take(ptr, n, dtype, shape):
-    out = np.frombuffer(C.string_at(ptr, n * np.dtype(dtype).itemsize * int(np.prod(shape[1:]))),
-                        dtype=dtype).reshape(shape).copy() if n else np.zeros(shape, dtype)
+    """Copy a library-allocated buffer into numpy and free it (no 2 GiB limit)."""
+    nbytes = n * np.dtype(dtype).itemsize * int(np.prod(shape[1:]))
+    if n:
+        raw = np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_uint8)), shape=(nbytes,))
+        out = raw.view(dtype).reshape(shape).copy()
+    else:
+        out = np.zeros(shape, dtype)
     lib().mp3g_free(ptr)
     return out
 
