@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-repeats", type=int, default=5)
     ap.add_argument("--gather", action="store_true", help="also time an RCCL PCM gather to rank 0")
+    ap.add_argument("--no-bitstream", action="store_true",
+                    help="skip the bitstream leg (host scan + GPU Huffman + DSP on real Layer III streams)")
     return ap.parse_args()
 
 
@@ -86,6 +88,82 @@ def build_workload(cfg, rank, seed_base=1, c5_copies=256):
                                                 "128 kbps CBR (synthetic; descriptors tiled from a "
                                                 "16,384-granule seeded pool)",
                                     "streams_per_gpu": 1024, "frames_per_stream": 1024}
+
+
+def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle):
+    """the same workload as real Layer III bitstreams
+    (synthetic writer, go-mp3_amd/csrc/synth_enc.cpp): host scan (headers,
+    side info, reservoir) on 16 threads, then on device-resident input the
+    Huffman kernel (scale factors + Huffman codes) and the DSP plan per step.
+    HIP events on the launch stream time the Huffman kernel alone and
+    Huffman + DSP."""
+    import torch
+    import mp3g
+    from concurrent.futures import ThreadPoolExecutor
+    from mp3g import synth
+    n_streams, n_frames = (1, 10000) if cfg == "c2" else (1024, 1024)
+    seed0 = 1 + 1000003 * rank
+    t = time.perf_counter()
+    with ThreadPoolExecutor(16) as ex:  # the writer releases the GIL (ctypes)
+        datas = list(ex.map(lambda k: synth.encode_stream(seed0 + k, n_frames), range(n_streams)))
+    writer_s = time.perf_counter() - t
+    t = time.perf_counter()
+    s = mp3g.scan_streams(datas, n_threads=16)
+    scan_s = time.perf_counter() - t
+    assert all(x == 7 for x in s["end_status"]), s["end_status"][:8]
+    n = len(s["granules"])
+    d_g = torch.from_numpy(s["granules"].view(np.uint8).copy()).to(dev)
+    d_j = torch.from_numpy(s["jobs"].view(np.uint8).copy()).to(dev)
+    d_m = torch.from_numpy(s["main_data"].copy()).to(dev)
+    d_c = torch.empty(n * 1152, dtype=torch.int16, device=dev)
+    d_p = torch.empty(n * 1152, dtype=torch.int16, device=dev)
+    idx = dev.index or 0
+    plan = mp3g.Plan(s["streams"], mode=mode, device=idx)
+    h = stream.cuda_stream
+
+    def huff():
+        mp3g.huffman_execute(d_j, n, d_m, d_g, d_c, stream=h, device=idx)
+
+    for _ in range(warmup):
+        huff()
+        plan.execute(d_g, d_c, d_p, stream=h)
+    torch.cuda.synchronize(dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    ev[0].record(stream)
+    for _ in range(steps):
+        huff()
+    ev[1].record(stream)
+    for _ in range(steps):
+        huff()
+        plan.execute(d_g, d_c, d_p, stream=h)
+    ev[2].record(stream)
+    torch.cuda.synchronize(dev)
+    huff_ms = ev[0].elapsed_time(ev[1]) / steps
+    both_ms = ev[1].elapsed_time(ev[2]) / steps
+    plan.close()
+    frames = n // 2
+    md = int(s["main_data"].nbytes)
+    out = {"workload": f"{cfg} as Layer III bitstreams: {n_streams} x {n_frames} frames, 44.1 kHz stereo "
+                       f"128 kbps CBR through the bit reservoir (synthetic writer synth_enc.cpp)",
+           "frames_per_s_device": round(frames / (both_ms * 1e-3), 1),
+           "huffman_plus_dsp_ms": round(both_ms, 4), "huffman_kernel_ms": round(huff_ms, 4),
+           "huffman_frames_per_s": round(frames / (huff_ms * 1e-3), 1),
+           # Huffman kernel algorithmic bytes: main data + 2 x 48-B jobs in;
+           # 2 x 1152 B coefficients + 2 x 63 B scale factors / count1 out per granule
+           "huffman_algorithmic_bytes_per_launch": md + n * (96 + 2304 + 126),
+           "huffman_algorithmic_gbps": round((md + n * (96 + 2304 + 126)) / (huff_ms * 1e-3) / 1e9, 2),
+           "main_data_bytes": md, "bitstream_bytes": int(sum(len(d) for d in datas)),
+           "host_scan_s": round(scan_s, 4), "host_scan_frames_per_s": round(frames / scan_s, 1),
+           "host_scan_threads": 16, "writer_s": round(writer_s, 2)}
+    if check_oracle:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle  # parity check of the timed output (checker only)
+        ost, opcm = oracle.decode_all(datas[0])
+        got = d_p.cpu().numpy()[:len(opcm) // 2]
+        want = np.frombuffer(opcm, np.int16)
+        out["max_dpcm_lsb_vs_oracle"] = int(np.abs(got.astype(np.int32) - want).max()) if ost == 0 and \
+            len(want) == n * 1152 else "oracle status %d" % ost
+    return out
 
 
 def profiled_traffic(cfg, kernel):
@@ -175,6 +253,12 @@ def main():
     main_res = res[args.mode]
     frames_rank = n_frames
 
+    bitstream = None
+    if not args.no_bitstream and args.config in ("c2", "c3"):
+        bitstream = bitstream_leg(args.config, rank, dev, stream,
+                                  mp3g.MODE_FAST if args.mode == "fast" else mp3g.MODE_EXACT,
+                                  args.steps, args.warmup, check_oracle=rank == 0 and args.config == "c2")
+
     gather_ms = None
     if args.gather and world > 1:
         torch.cuda.synchronize(dev)
@@ -216,6 +300,8 @@ def main():
         }
         if gather_ms is not None:
             out["gather_ms"] = round(gather_ms, 3)
+        if bitstream is not None:
+            out["bitstream"] = bitstream
         if world == 1 and not args.no_cpu_baseline and args.config == "c2":
             sys.path.insert(0, os.path.join(REPO, "oracle"))
             import oracle  # CPU baseline leg + parity check of the timed output

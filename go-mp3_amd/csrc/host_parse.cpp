@@ -609,5 +609,162 @@ St FrameParser::next(Source& s, ParsedFrame* out) {
   return St::kOk;
 }
 
+// ---- frame.Read without the main-data decode ----------
+namespace {
+
+// Bit position after a job's scale factors: the reads of maindata.go:132-279
+// in order, each skipped (no advance) when it would pass the end (bits.go:58-68).
+int64_t sf_end(int64_t pos, int64_t end, const mp3g_hjob& j) {
+  auto rd = [&](int n) {
+    if (n > 0 && pos + n <= end) pos += n;
+  };
+  switch (j.sf_kind) {
+    case MP3G_SF_MPEG1_LONG:
+      for (int part = 0; part < 4; part++) {
+        if ((j.scfsi >> part) & 1) continue;
+        for (int k = 0; k < (part == 0 ? 6 : 5); k++) rd(part < 2 ? j.slen[0] : j.slen[1]);
+      }
+      break;
+    case MP3G_SF_MPEG1_SHORT:
+    case MP3G_SF_MPEG1_MIXED:
+      if (j.sf_kind == MP3G_SF_MPEG1_MIXED)
+        for (int sfb = 0; sfb < 8; sfb++) rd(j.slen[0]);
+      for (int sfb = j.sf_kind == MP3G_SF_MPEG1_MIXED ? 3 : 0; sfb < 12; sfb++)
+        for (int w = 0; w < 3; w++) rd(sfb < 6 ? j.slen[0] : j.slen[1]);
+      break;
+    case MP3G_SF_MPEG2_LONG:
+    case MP3G_SF_MPEG2_SHORT:
+      for (int part = 0; part < 4; part++)
+        for (int k = 0; k < j.nsf[part]; k++) rd(j.slen[part]);
+      break;
+  }
+  return pos;
+}
+
+}  // namespace
+
+St FrameScanner::next(Source& s, ScannedFrame* out, std::vector<uint8_t>* md) {
+  // header, CRC, side info and sizes exactly as FrameParser::next
+  uint32_t h;
+  int64_t pos = s.pos;
+  St st = read_header(s, &pos, &h);
+  if (st != St::kOk) return st;
+  if (h_protection(h) == 0) {
+    uint8_t crc[2];
+    bool sr;
+    if (s.read_full(crc, 2, &sr) < 2) return sr ? St::kEof : St::kErr;
+  }
+  if (h_id(h) == 0) return St::kErr;
+  if (h_layer(h) != 1) return St::kErr;
+  SideInfo si;
+  st = read_side_info(s, h, &si);
+  if (st != St::kOk) return st;
+  const int fsize = header_frame_size(h);
+  if (fsize > 2000) return St::kErr;
+  int size = fsize - h_side_info_size(h) - 4;
+  if (h_protection(h) == 0) size -= 2;
+  if (size > 1500) return St::kErr;
+  if (size < 0) return St::kPanic;
+
+  // reservoir (maindata.go:290-323): the frame's bit buffer is the suffix of
+  // the main-data concatenation starting at `vstart` -- the tail of the
+  // previous buffer, all of it on an underflow, nothing without a previous
+  // frame.  (An underflow needs main_data_begin > the previous buffer, and
+  // main_data_begin < 512, so a bit buffer never exceeds ~2 KB.)
+  const int64_t g0 = (int64_t)md->size();
+  const int offset = si.main_data_begin;
+  const bool underflow = have_prev_ && offset > g0 - prev_start_;
+  const int64_t vstart = !have_prev_ ? g0 : underflow ? prev_start_ : g0 - offset;
+  md->resize((size_t)(g0 + size));
+  bool sr;
+  if (s.read_full(md->data() + g0, size, &sr) < size) {
+    md->resize((size_t)g0);
+    return sr ? St::kEof : St::kErr;
+  }
+  const int64_t end = (int64_t)md->size() * 8;
+
+  const int lsf = h_lsf(h), nch = h_nch(h), ng = header_granules(h);
+  out->header = h;
+  out->start = pos;
+  out->n_granules = ng;
+  std::memset(out->gran, 0, sizeof out->gran);
+  std::memset(out->job, 0, sizeof out->job);
+  int64_t bit = vstart * 8;  // m.BitPos() as an absolute position
+  for (int gr = 0; gr < ng; gr++) {
+    mp3g_granule& G = out->gran[gr];
+    G.header = h;
+    G.gr = (uint32_t)gr;
+    for (int ch = 0; ch < nch; ch++) {
+      mp3g_channel& c = G.ch[ch];
+      c.global_gain = (uint8_t)si.global_gain[gr][ch];
+      c.scalefac_scale = (uint8_t)si.scalefac_scale[gr][ch];
+      c.preflag = (uint8_t)si.preflag[gr][ch];
+      c.win_switch_flag = (uint8_t)si.win_switch_flag[gr][ch];
+      c.block_type = (uint8_t)si.block_type[gr][ch];
+      c.mixed_block_flag = (uint8_t)si.mixed_block_flag[gr][ch];
+      for (int w = 0; w < 3; w++) c.subblock_gain[w] = (uint8_t)si.subblock_gain[gr][ch][w];
+
+      mp3g_hjob& J = out->job[gr][ch];
+      J.part2_start = (uint64_t)bit;
+      J.bit_end = (uint64_t)end;
+      J.part2_3_length = (uint16_t)si.part2_3_length[gr][ch];
+      J.big_values = (uint16_t)si.big_values[gr][ch];
+      for (int r = 0; r < 3; r++) J.table_select[r] = (uint8_t)si.table_select[gr][ch][r];
+      J.count1_table = (uint8_t)si.count1_table_select[gr][ch];
+      // region boundaries (maindata/huffman.go:39-64)
+      const bool shortblk = si.win_switch_flag[gr][ch] == 1 && si.block_type[gr][ch] == 2;
+      if (shortblk) {
+        J.region1_start = 36;
+        J.region2_start = 576;
+      } else {
+        const int* l = kSfbLong[lsf][h_sfreq(h)];
+        J.region1_start = (uint16_t)l[si.region0_count[gr][ch] + 1];  // index <= 16 < 23
+        const int j = si.region0_count[gr][ch] + si.region1_count[gr][ch] + 2;
+        J.region2_start = (uint16_t)(j >= 23 ? 576 : l[j]);
+      }
+      if (lsf) {  // getScaleFactorsMpeg2 (maindata.go:132-179)
+        int slen = kSlen2.v[si.scalefac_compress[0][ch]];
+        c.preflag = (uint8_t)((slen >> 15) & 1);
+        int blk = 0;
+        if (si.block_type[0][ch] == 2) blk = si.mixed_block_flag[0][ch] != 0 ? 2 : 1;
+        if (blk == 2) return St::kPanic;  // 38 scale factors: index out of range in the reference
+        const int row = (slen >> 12) & 7;
+        for (int part = 0; part < 4; part++) {
+          J.slen[part] = (uint8_t)(slen & 7);
+          slen >>= 3;
+          J.nsf[part] = (uint8_t)kNsfbMpeg2[blk][row][part];
+        }
+        J.sf_kind = blk ? MP3G_SF_MPEG2_SHORT : MP3G_SF_MPEG2_LONG;
+      } else {  // getScaleFactorsMpeg1 (maindata.go:190-279)
+        J.slen[0] = (uint8_t)kSlenMpeg1[si.scalefac_compress[gr][ch]][0];
+        J.slen[1] = (uint8_t)kSlenMpeg1[si.scalefac_compress[gr][ch]][1];
+        J.sf_kind = !shortblk                            ? MP3G_SF_MPEG1_LONG
+                    : si.mixed_block_flag[gr][ch] != 0 ? MP3G_SF_MPEG1_MIXED
+                                                       : MP3G_SF_MPEG1_SHORT;
+        if (gr == 1 && J.sf_kind == MP3G_SF_MPEG1_LONG) {
+          for (int part = 0; part < 4; part++) J.scfsi |= (uint8_t)((si.scfsi[ch][part] == 1) << part);
+          if (J.scfsi) {
+            const mp3g_hjob& J0 = out->job[0][ch];
+            J.scf0_delta = (uint32_t)(J.part2_start - J0.part2_start);
+            J.sf0_kind = J0.sf_kind;
+            J.sf0_slen[0] = J0.slen[0];
+            J.sf0_slen[1] = J0.slen[1];
+          }
+        }
+      }
+      const int64_t after_sf = sf_end(bit, end, J);
+      if (J.part2_3_length == 0) {
+        bit = after_sf;  // readHuffman returns before m.SetPos (maindata/huffman.go:29-34)
+      } else {
+        if (J.big_values > 288) return St::kErr;  // "isPos was too big" (maindata/huffman.go:67-70)
+        bit += J.part2_3_length;                   // m.SetPos(bitPosEnd + 1)
+      }
+    }
+  }
+  prev_start_ = vstart;
+  have_prev_ = true;
+  return St::kOk;
+}
+
 }  // namespace host
 }  // namespace mp3g

@@ -65,6 +65,34 @@ class FrameParser {
   std::vector<uint8_t> md_;       // scratch
 };
 
+// frame.Read split at the bit reservoir: everything
+// but the scale factors and Huffman codes, which the device decodes
+// (huffman_dev.hip) from one job per (granule, channel).
+struct ScannedFrame {
+  uint32_t header = 0;
+  int64_t start = 0;
+  int n_granules = 0;
+  mp3g_granule gran[2];  // side-info fields; scale factors and count1 zero
+  mp3g_hjob job[2][2];   // [gr][ch]; bit positions in the scanner's main-data buffer
+};
+
+class FrameScanner {
+ public:
+  // Parses the next frame's header and side info and appends its main-data
+  // bytes to *md; the same statuses, at the same source positions, as
+  // FrameParser::next on the same input.
+  St next(Source& src, ScannedFrame* out, std::vector<uint8_t>* md);
+  void reset() { have_prev_ = false; }  // frame.Read(source, pos, nil)
+  // First byte of *md the next frame's bit buffer can reach back to.
+  int64_t live_start(const std::vector<uint8_t>& md) const { return have_prev_ ? prev_start_ : (int64_t)md.size(); }
+  // Rebases after the caller dropped the first n bytes of *md.
+  void drop(int64_t n) { prev_start_ -= n; }
+
+ private:
+  bool have_prev_ = false;
+  int64_t prev_start_ = 0;  // byte offset in *md of the previous frame's bit buffer
+};
+
 // frameheader.Read: sync search from the source position.
 St read_header(Source& s, int64_t* pos_io, uint32_t* out);
 

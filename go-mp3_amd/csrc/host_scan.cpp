@@ -1,0 +1,217 @@
+// host_scan.cpp -- batch entry points of the GPU main-data path (SURVEY.md 8f
+// row f1): mp3g_scan_streams (host: tags, headers, side info, reservoir --
+// host_parse.cpp FrameScanner) and mp3g_decode_streams (bitstreams in, PCM
+// out: the scan, then Huffman + DSP on the device).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <thread>
+#include <vector>
+
+#include "../../include/mp3g.h"
+#include "abi_util.h"
+#include "host_parse.h"
+
+using namespace mp3g;
+using host::St;
+
+struct mp3g_scan {
+  std::vector<mp3g_granule> gran;
+  std::vector<mp3g_hjob> jobs;
+  std::vector<uint8_t> md;
+  std::vector<mp3g_stream> streams;
+  std::vector<int> status;
+};
+
+namespace {
+
+int to_status(St s) {
+  switch (s) {
+    case St::kOk: return MP3G_OK;
+    case St::kEof: return MP3G_EOF;
+    case St::kErr: return MP3G_ERR_PARSE;
+    case St::kPanic: return MP3G_ERR_UNSUPPORTED;
+  }
+  return MP3G_ERR_PARSE;
+}
+
+struct StreamScan {
+  std::vector<mp3g_granule> gran;
+  std::vector<mp3g_hjob> jobs;  // positions relative to md
+  std::vector<uint8_t> md;
+  St end = St::kOk;
+};
+
+// NewDecoder + reading to the end (as host_decoder.cpp parse_all).
+void scan_all(const uint8_t* data, size_t len, StreamScan* out) {
+  host::Source src;
+  src.data = data;
+  src.len = (int64_t)len;
+  St st = src.skip_tags();
+  if (st != St::kOk) {
+    out->end = st;
+    return;
+  }
+  out->md.reserve(len);
+  host::FrameScanner sc;
+  host::ScannedFrame f;
+  for (;;) {
+    st = sc.next(src, &f, &out->md);
+    if (st != St::kOk) break;
+    for (int gr = 0; gr < f.n_granules; gr++) {
+      out->gran.push_back(f.gran[gr]);
+      out->jobs.push_back(f.job[gr][0]);
+      out->jobs.push_back(f.job[gr][1]);
+    }
+  }
+  out->end = st;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mp3g_scan_streams(uint32_t n_streams, const uint8_t* const* datas, const size_t* lens, int n_threads,
+                      mp3g_scan** out) {
+  if (!out || (n_streams && (!datas || !lens))) return abi_fail(MP3G_ERR_INVALID_ARGUMENT, "null argument");
+  *out = nullptr;
+  mp3g_scan* s = new (std::nothrow) mp3g_scan;
+  if (!s) return abi_fail(MP3G_ERR_OUT_OF_MEMORY, "scan");
+  std::vector<StreamScan> per(n_streams);
+  std::atomic<uint32_t> next{0};
+  auto work = [&]() {
+    for (uint32_t k; (k = next.fetch_add(1)) < n_streams;) scan_all(datas[k], lens[k], &per[k]);
+  };
+  const int nt = std::max(1, std::min<int>(n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency(),
+                                           (int)std::max<uint32_t>(1, n_streams)));
+  std::vector<std::thread> pool;
+  for (int t = 1; t < nt; t++) pool.emplace_back(work);
+  work();
+  for (auto& t : pool) t.join();
+  uint64_t ng = 0, nmd = 0;
+  for (const StreamScan& p : per) {
+    ng += p.gran.size();
+    nmd += (p.md.size() + 15) & ~(size_t)15;  // each stream's bytes 16-B aligned
+  }
+  s->gran.resize(ng);
+  s->jobs.resize(2 * ng);
+  s->md.assign(nmd + 16, 0);  // + padding for the device's 32-bit window loads
+  s->streams.resize(n_streams);
+  s->status.resize(n_streams);
+  uint64_t g = 0, m = 0;
+  for (uint32_t k = 0; k < n_streams; k++) {
+    const StreamScan& p = per[k];
+    s->streams[k].first_granule = g;
+    s->streams[k].n_granules = (uint32_t)p.gran.size();
+    s->streams[k].flags = 0;
+    s->status[k] = to_status(p.end);
+    if (!p.gran.empty()) std::memcpy(&s->gran[g], p.gran.data(), p.gran.size() * sizeof(mp3g_granule));
+    for (size_t i = 0; i < p.jobs.size(); i++) {
+      mp3g_hjob J = p.jobs[i];
+      if (J.sf_kind != MP3G_SF_NONE) {
+        J.part2_start += 8 * m;
+        J.bit_end += 8 * m;
+      }
+      s->jobs[2 * g + i] = J;
+    }
+    if (!p.md.empty()) std::memcpy(&s->md[m], p.md.data(), p.md.size());
+    g += p.gran.size();
+    m += (p.md.size() + 15) & ~(size_t)15;
+  }
+  *out = s;
+  return MP3G_OK;
+}
+
+int mp3g_scan_buffers(const mp3g_scan* s, uint64_t* n_granules, uint64_t* main_data_bytes,
+                      const mp3g_granule** granules, const mp3g_hjob** jobs, const uint8_t** main_data,
+                      const mp3g_stream** streams, const int** end_status) {
+  if (!s) return abi_fail(MP3G_ERR_INVALID_ARGUMENT, "null scan");
+  if (n_granules) *n_granules = s->gran.size();
+  if (main_data_bytes) *main_data_bytes = s->md.size();
+  if (granules) *granules = s->gran.data();
+  if (jobs) *jobs = s->jobs.data();
+  if (main_data) *main_data = s->md.data();
+  if (streams) *streams = s->streams.data();
+  if (end_status) *end_status = s->status.data();
+  return MP3G_OK;
+}
+
+void mp3g_scan_free(mp3g_scan* s) { delete s; }
+
+int mp3g_decode_streams(int device, uint32_t n_streams, const uint8_t* const* datas, const size_t* lens,
+                        int n_threads, uint32_t mode, int16_t** pcm, uint64_t* n_granules, mp3g_stream* streams,
+                        int* end_status) {
+  if (!pcm || !n_granules || (n_streams && (!streams || !end_status)))
+    return abi_fail(MP3G_ERR_INVALID_ARGUMENT, "null argument");
+  *pcm = nullptr;
+  *n_granules = 0;
+  mp3g_scan* s = nullptr;
+  int rc = mp3g_scan_streams(n_streams, datas, lens, n_threads, &s);
+  if (rc) return rc;
+  const size_t n = s->gran.size();
+  if (n_streams) {
+    std::memcpy(streams, s->streams.data(), n_streams * sizeof(mp3g_stream));
+    std::memcpy(end_status, s->status.data(), n_streams * sizeof(int));
+  }
+  int16_t* host_pcm = static_cast<int16_t*>(std::malloc(std::max<size_t>(1, n) * MP3G_PCM_BYTES_PER_GRANULE));
+  if (!host_pcm) {
+    mp3g_scan_free(s);
+    return abi_fail(MP3G_ERR_OUT_OF_MEMORY, "pcm");
+  }
+  if (n == 0) {
+    mp3g_scan_free(s);
+    *pcm = host_pcm;
+    return MP3G_OK;
+  }
+  mp3g_plan* plan = nullptr;
+  rc = mp3g_plan_create(device, s->streams.data(), n_streams, 0, mode, &plan);
+  if (rc) {
+    mp3g_scan_free(s);
+    std::free(host_pcm);
+    return rc;
+  }
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  void *dg = nullptr, *dj = nullptr, *dm = nullptr, *dc = nullptr, *dp = nullptr;
+  hipStream_t st = nullptr;
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipMalloc(&dg, n * sizeof(mp3g_granule));
+  if (e == hipSuccess) e = hipMalloc(&dj, 2 * n * sizeof(mp3g_hjob));
+  if (e == hipSuccess) e = hipMalloc(&dm, s->md.size());
+  if (e == hipSuccess) e = hipMalloc(&dc, n * MP3G_COEF_PER_GRANULE * sizeof(int16_t));
+  if (e == hipSuccess) e = hipMalloc(&dp, n * MP3G_PCM_BYTES_PER_GRANULE);
+  if (e == hipSuccess) e = hipMemcpyAsync(dg, s->gran.data(), n * sizeof(mp3g_granule), hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(dj, s->jobs.data(), 2 * n * sizeof(mp3g_hjob), hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(dm, s->md.data(), s->md.size(), hipMemcpyHostToDevice, st);
+  rc = e == hipSuccess ? MP3G_OK : abi_fail(MP3G_ERR_DEVICE, "decode_streams: device buffers / H2D");
+  if (rc == MP3G_OK)
+    rc = mp3g_huffman_execute(device, (const mp3g_hjob*)dj, n, (const uint8_t*)dm, (mp3g_granule*)dg,
+                              (int16_t*)dc, st);
+  if (rc == MP3G_OK)
+    rc = mp3g_plan_execute(plan, (const mp3g_granule*)dg, (const int16_t*)dc, nullptr, nullptr, (int16_t*)dp, st);
+  if (rc == MP3G_OK) {
+    e = hipMemcpyAsync(host_pcm, dp, n * MP3G_PCM_BYTES_PER_GRANULE, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) rc = abi_fail(MP3G_ERR_DEVICE, "decode_streams: decode / D2H");
+  }
+  for (void* q : {dg, dj, dm, dc, dp})
+    if (q) (void)hipFree(q);
+  if (st) (void)hipStreamDestroy(st);
+  if (prev >= 0) (void)hipSetDevice(prev);
+  mp3g_plan_destroy(plan);
+  mp3g_scan_free(s);
+  if (rc) {
+    std::free(host_pcm);
+    return rc;
+  }
+  *pcm = host_pcm;
+  *n_granules = n;
+  return MP3G_OK;
+}
+
+}  // extern "C"

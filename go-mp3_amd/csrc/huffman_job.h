@@ -1,0 +1,257 @@
+// huffman_job.h -- one (granule, channel) job of the GPU main-data decode
+// (huffman_dev.hip): scale factors (maindata.go:119-288)
+// and Huffman codes (maindata/huffman.go:27-138, huffman/huffman.go:348-419)
+// of one channel, read straight out of the concatenated main-data buffer.
+//
+// Bit semantics are the reference's bits.Bits (bits.go:45-77): a read that
+// would pass the end of the frame's main-data buffer returns 0 and does not
+// advance.  The 64-bit window is masked with zeros from bit_end on, and every
+// advance is clamped exactly as the reference's bit-by-bit tree walk and
+// Bit()/Bits() calls advance.
+//
+// __host__ __device__: the kernel runs it per lane; tests/hjob_host.hip
+// compiles the same code for the CPU to check the job decomposition against
+// the host parse without a GPU (test infrastructure, not a product path).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../../include/mp3g.h"
+#include "huff_lut.h"
+
+#define MP3G_HD_INLINE __host__ __device__ __forceinline__
+
+namespace mp3g {
+namespace huff {
+
+// Big-endian reader over the main-data buffer.  Positions are 32-bit offsets
+// from `w`, a 32-bit-aligned bit position at or before every bit the job
+// reads (a frame's bit buffer spans at most a few KiB: host_parse.cpp).
+struct Reader {
+  const uint32_t* w;
+  uint32_t end;   // bit_end - base (0 if the job starts past its buffer)
+  uint32_t wpos;  // bit offset of win's MSB (multiple of 32)
+  uint32_t pos;
+  uint32_t nxt;   // bits [wpos + 64, wpos + 96)
+  uint64_t win;   // bits [wpos, wpos + 64)
+
+  MP3G_HD_INLINE uint32_t word(uint32_t bit) const {  // bit % 32 == 0
+    if (bit >= end) return 0u;
+    const uint32_t v = __builtin_bswap32(w[bit >> 5]);
+    const uint32_t rem = end - bit;
+    return rem < 32u ? v & (~0u << (32u - rem)) : v;
+  }
+  MP3G_HD_INLINE void seek(uint32_t p) {
+    pos = p;
+    wpos = p & ~31u;
+    win = ((uint64_t)word(wpos) << 32) | word(wpos + 32);
+    nxt = word(wpos + 64);
+  }
+  // bits [pos, pos + 32) in the window: every read is <= 19 bits, so one step
+  // restores pos - wpos < 32
+  MP3G_HD_INLINE void refill() {
+    if (pos - wpos >= 32u) {
+      win = (win << 32) | nxt;
+      wpos += 32;
+      nxt = word(wpos + 64);
+    }
+  }
+  MP3G_HD_INLINE uint32_t peek() const { return (uint32_t)((win << (pos - wpos)) >> 32); }
+  // bits.Bits(n), 1 <= n <= 13: 0 and no advance if it would pass the end
+  MP3G_HD_INLINE uint32_t bits(int n) {
+    refill();
+    if (pos + (uint32_t)n > end) return 0u;
+    const uint32_t v = peek() >> (32 - n);
+    pos += (uint32_t)n;
+    return v;
+  }
+  // bits.Bit()
+  MP3G_HD_INLINE uint32_t bit() {
+    refill();
+    if (pos >= end) return 0u;
+    const uint32_t v = peek() >> 31;
+    pos++;
+    return v;
+  }
+};
+
+// huffman.Decode's tree walk: the leaf the next bits reach (zeros past the
+// end) and the advance of its Bit() calls, min(len, end - pos).
+MP3G_HD_INLINE uint32_t decode_xy(Reader& r, const uint32_t* T, uint32_t root) {
+  r.refill();
+  const uint32_t p = r.peek();
+  int used = (int)(root >> 24);
+  uint32_t e = T[(root & 0xffffffu) + (p >> (32 - used))];
+  while (e & 0x80000000u) {
+    const int wd = (int)((e >> 24) & 15u);
+    e = T[(e & 0xffffffu) + ((p << used) >> (32 - wd))];
+    used += wd;
+  }
+  const uint32_t len = (e >> 8) & 31u;
+  if (r.pos < r.end) r.pos = r.pos + len < r.end ? r.pos + len : r.end;
+  return e & 255u;
+}
+
+// 16-byte staging of consecutive line pairs (lines are produced strictly in
+// order from 0, two at a time).
+struct LineWriter {
+  int16_t* row;
+  uint32_t b0, b1, b2, b3;
+  MP3G_HD_INLINE void put(int i, int a, int b) {
+    const uint32_t v = (uint32_t)(uint16_t)(int16_t)a | ((uint32_t)(uint16_t)(int16_t)b << 16);
+    const int slot = (i >> 1) & 3;
+    b0 = slot == 0 ? v : b0;
+    b1 = slot == 1 ? v : b1;
+    b2 = slot == 2 ? v : b2;
+    b3 = slot == 3 ? v : b3;
+    if (slot == 3) {
+      *reinterpret_cast<uint4*>(row + (i & ~7)) = make_uint4(b0, b1, b2, b3);
+      b0 = b1 = b2 = b3 = 0u;
+    }
+  }
+  // flushes the pending block; lines [i, 576) zero (i even)
+  MP3G_HD_INLINE void finish(int i) {
+    if (i & 7) *reinterpret_cast<uint4*>(row + (i & ~7)) = make_uint4(b0, b1, b2, b3);
+    for (int k = (i + 7) & ~7; k < 576; k += 8) *reinterpret_cast<uint4*>(row + k) = make_uint4(0u, 0u, 0u, 0u);
+  }
+};
+
+// MPEG-1 long-block scale factors (maindata.go:233-279): parts in `read` are
+// read from the stream, parts in `store` are written to sfl.
+MP3G_HD_INLINE void sf_mpeg1_long(Reader& r, int slen1, int slen2, uint32_t read, uint32_t store,
+                                              uint8_t* sfl) {
+#pragma unroll
+  for (int part = 0; part < 4; part++) {
+    if (!((read >> part) & 1u)) continue;
+    const int lo = part == 0 ? 0 : part == 1 ? 6 : part == 2 ? 11 : 16;
+    const int hi = part == 0 ? 6 : part == 1 ? 11 : part == 2 ? 16 : 21;
+    const int nb = part < 2 ? slen1 : slen2;
+    const bool st = (store >> part) & 1u;
+    for (int sfb = lo; sfb < hi; sfb++) {
+      const uint32_t v = nb ? r.bits(nb) : 0u;
+      if (st) sfl[sfb] = (uint8_t)v;
+    }
+  }
+}
+
+// Decodes job j (= 2 * granule + channel): scale factors and count1 into
+// gran[j / 2].ch[j % 2], the 576 lines into coef[j * 576 ..].  T / s_root /
+// s_lin: the HuffLut entries, roots and linbits (LDS on the device).
+MP3G_HD_INLINE void decode_job(const mp3g_hjob& J, uint64_t j, const uint8_t* md, mp3g_granule* gran,
+                               int16_t* coef, const uint32_t* T, const uint32_t* s_root, const uint32_t* s_lin) {
+  int16_t* row = coef + j * MP3G_LINES;
+  LineWriter out{row, 0u, 0u, 0u, 0u};
+  if (J.sf_kind == MP3G_SF_NONE) {  // absent channel of a mono granule
+    out.finish(0);
+    return;
+  }
+  mp3g_channel& C = gran[j >> 1].ch[j & 1];
+  uint8_t* sfl = C.scalefac_l;
+  uint8_t* sfs = &C.scalefac_s[0][0];
+
+  const uint64_t base = (J.part2_start - J.scf0_delta) & ~31ull;
+  Reader r;
+  r.w = reinterpret_cast<const uint32_t*>(md + (base >> 3));
+  r.end = J.bit_end > base ? (uint32_t)(J.bit_end - base) : 0u;
+  const uint32_t part2 = (uint32_t)(J.part2_start - base);
+
+  // ---- scale factors ----
+  const int slen1 = J.slen[0], slen2 = J.slen[1];
+  switch (J.sf_kind) {
+    case MP3G_SF_MPEG1_LONG:
+      if (J.scfsi) {
+        // granule 1 copies the scfsi parts from granule 0 (maindata.go:239-278):
+        // re-read them from granule 0's part 2 (zero where granule 0 has none)
+        r.seek(part2 - J.scf0_delta);
+        if (J.sf0_kind == MP3G_SF_MPEG1_LONG) {
+          sf_mpeg1_long(r, J.sf0_slen[0], J.sf0_slen[1], 15u, J.scfsi, sfl);
+        } else if (J.sf0_kind == MP3G_SF_MPEG1_MIXED) {
+          const int nb = J.sf0_slen[0];
+          for (int sfb = 0; sfb < 8; sfb++) {
+            const uint32_t v = nb ? r.bits(nb) : 0u;
+            if ((J.scfsi >> (sfb < 6 ? 0 : 1)) & 1u) sfl[sfb] = (uint8_t)v;
+          }
+        }
+      }
+      r.seek(part2);
+      sf_mpeg1_long(r, slen1, slen2, ~(uint32_t)J.scfsi & 15u, ~(uint32_t)J.scfsi & 15u, sfl);
+      break;
+    case MP3G_SF_MPEG1_SHORT:
+    case MP3G_SF_MPEG1_MIXED: {
+      r.seek(part2);
+      int s0 = 0;
+      if (J.sf_kind == MP3G_SF_MPEG1_MIXED) {
+        for (int sfb = 0; sfb < 8; sfb++) sfl[sfb] = (uint8_t)(slen1 ? r.bits(slen1) : 0u);
+        s0 = 3;
+      }
+      for (int sfb = s0; sfb < 12; sfb++) {
+        const int nb = sfb < 6 ? slen1 : slen2;
+        for (int win = 0; win < 3; win++) sfs[3 * sfb + win] = (uint8_t)(nb ? r.bits(nb) : 0u);
+      }
+      break;
+    }
+    default: {  // MPEG-2 (maindata.go:132-179): nsf[part] factors of slen[part] bits
+      r.seek(part2);
+      const bool lng = J.sf_kind == MP3G_SF_MPEG2_LONG;
+      int k = 0;
+      for (int part = 0; part < 4; part++) {
+        const int nb = J.slen[part];
+        for (int n = 0; n < (int)J.nsf[part]; n++, k++) {
+          const uint8_t v = (uint8_t)(nb ? r.bits(nb) : 0u);
+          if (lng) {
+            if (k < 22) sfl[k] = v;
+          } else if (k < 39) {
+            sfs[k] = v;
+          }
+        }
+      }
+      break;
+    }
+  }
+
+  // ---- Huffman (maindata/huffman.go:27-138) ----
+  int i = 0, count1 = 0;
+  const uint32_t p23 = J.part2_3_length;
+  if (p23) {
+    const uint32_t pend = part2 + p23 - 1;  // bitPosEnd
+    const int bv2 = 2 * (int)J.big_values;  // <= 576 (the scan rejects more)
+    const int r1 = J.region1_start, r2 = J.region2_start;
+    for (; i < bv2; i += 2) {
+      const int tbl = i < r1 ? J.table_select[0] : i < r2 ? J.table_select[1] : J.table_select[2];
+      const uint32_t root = s_root[tbl];
+      int x = 0, y = 0;
+      if (root) {
+        const uint32_t xy = decode_xy(r, T, root);
+        x = (int)(xy >> 4);
+        y = (int)(xy & 15u);
+        const int lb = (int)s_lin[tbl];
+        if (lb && x == 15) x += (int)r.bits(lb);
+        if (x && r.bit()) x = -x;
+        if (lb && y == 15) y += (int)r.bits(lb);
+        if (y && r.bit()) y = -y;
+      }
+      out.put(i, x, y);
+    }
+    const uint32_t qroot = s_root[32 + J.count1_table];
+    while (i <= 572 && r.pos <= pend) {
+      const uint32_t q = decode_xy(r, T, qroot) & 15u;
+      int v = (int)((q >> 3) & 1u), w = (int)((q >> 2) & 1u), x = (int)((q >> 1) & 1u), y = (int)(q & 1u);
+      if (v && r.bit()) v = -v;
+      if (w && r.bit()) w = -w;
+      if (x && r.bit()) x = -x;
+      if (y && r.bit()) y = -y;
+      out.put(i, v, w);
+      out.put(i + 2, x, y);
+      i += 4;
+    }
+    count1 = i;
+    if (r.pos > pend + 1) count1 = i >= 4 ? i - 4 : 0;  // the last word overran its part
+  }
+  out.finish(i);
+  for (int k = count1; k < i; k++) row[k] = 0;  // lines the overrun check removed
+  C.count1 = (uint16_t)count1;
+}
+
+}  // namespace huff
+}  // namespace mp3g

@@ -6,6 +6,7 @@
 
 #include "../../include/mp3g.h"
 #include "dsp_tables.h"
+#include "huff_lut.h"
 
 namespace mp3g {
 
@@ -36,6 +37,10 @@ hipError_t launch_granule(int variant, const ChunkDesc* d_chunks, uint32_t n_chu
                           const mp3g_granule* d_gran, const int16_t* d_coef,
                           const mp3g_state* d_state_in, mp3g_state* d_state_out, int16_t* d_pcm,
                           hipStream_t stream);
+
+// Main-data decode (huffman_dev.hip): one lane per (granule, channel) job.
+hipError_t launch_huffman(const mp3g_hjob* d_jobs, uint64_t n_jobs, const uint8_t* d_md, mp3g_granule* d_gran,
+                          int16_t* d_coef, hipStream_t stream);
 
 // Diagnostic: fast kernel with per-phase s_memtime sums (8 per chunk) in d_stamps.
 constexpr int kFastPhases = 8;

@@ -3,8 +3,9 @@
 // Holds the constant tables (uploaded once per device) and both exact-mode
 // kernels: v1 (granule_exact.hip, the straightforward per-phase version, kept
 // as an on-device cross-check) and v2 (granule_fused.hip, the production
-// kernel), plus the fast-mode kernel v3 (granule_fast.hip, +-1 LSB).  One TU
-// so all of them reach g_tab / g_fast without relocatable device code.
+// kernel), the fast-mode kernel v3 (granule_fast.hip, +-1 LSB) and the
+// main-data (scale factor + Huffman) kernel (huffman_dev.hip).  One TU
+// so all of them reach g_tab / g_fast / g_huff without relocatable device code.
 #include <hip/hip_runtime.h>
 
 #include "../../include/mp3g.h"
@@ -16,12 +17,14 @@
 namespace mp3g {
 __device__ DspTables g_tab;
 __constant__ FastTables g_fast;
+__device__ HuffLut g_huff;
 }  // namespace mp3g
 
 #include "granule_common.hip"
 #include "granule_exact.hip"
 #include "granule_fused.hip"
 #include "granule_fast.hip"
+#include "huffman_dev.hip"
 
 namespace mp3g {
 
@@ -30,7 +33,16 @@ hipError_t upload_tables(const DspTables& tables) {
   if (e != hipSuccess) return e;
   FastTables fast;
   build_fast_tables(tables, &fast);
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_fast), &fast, sizeof(FastTables), 0, hipMemcpyHostToDevice);
+  e = hipMemcpyToSymbol(HIP_SYMBOL(g_fast), &fast, sizeof(FastTables), 0, hipMemcpyHostToDevice);
+  if (e != hipSuccess) return e;
+  HuffLut* lut = new HuffLut;
+  if (!build_huff_lut(lut)) {
+    delete lut;
+    return hipErrorInvalidValue;
+  }
+  e = hipMemcpyToSymbol(HIP_SYMBOL(g_huff), lut, sizeof(HuffLut), 0, hipMemcpyHostToDevice);
+  delete lut;
+  return e;
 }
 
 hipError_t launch_granule(int variant, const ChunkDesc* d_chunks, uint32_t n_chunks,

@@ -285,6 +285,18 @@ int mp3g_plan_execute(mp3g_plan* p, const mp3g_granule* d_gran, const int16_t* d
   return MP3G_OK;
 }
 
+int mp3g_huffman_execute(int device, const mp3g_hjob* d_jobs, uint64_t n_granules, const uint8_t* d_md,
+                         mp3g_granule* d_gran, int16_t* d_coef, void* hip_stream) {
+  if (n_granules == 0) return MP3G_OK;
+  if (!d_jobs || !d_md || !d_gran || !d_coef) return fail(MP3G_ERR_INVALID_ARGUMENT, "null device buffer");
+  DeviceGuard guard(device);
+  if (guard.err != hipSuccess) return fail(MP3G_ERR_NO_DEVICE, "hipSetDevice", guard.err);
+  int st = ensure_device(device);
+  if (st) return st;
+  HIP_TRY(launch_huffman(d_jobs, 2 * n_granules, d_md, d_gran, d_coef, static_cast<hipStream_t>(hip_stream)));
+  return MP3G_OK;
+}
+
 int mp3g_plan_debug_phases(mp3g_plan* p, const mp3g_granule* d_gran, const int16_t* d_coef, int16_t* d_pcm,
                            uint64_t* out_cycles, void* hip_stream) {
   if (!p || !out_cycles) return fail(MP3G_ERR_INVALID_ARGUMENT, "null argument");

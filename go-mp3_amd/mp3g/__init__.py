@@ -15,7 +15,7 @@ import numpy as np
 __all__ = ["CHANNEL_DTYPE", "GRANULE_DTYPE", "STREAM_DTYPE", "STATE_DTYPE", "MODE_EXACT",
            "MODE_FAST", "FLAG_CHECKED", "FLAG_KERNEL_V1", "STATE_IN", "STATE_OUT", "Mp3gError", "lib", "lib_path",
            "decode_host", "validate", "Plan", "device_count", "streams_for", "parse_stream",
-           "parse_streams", "Decoder"]
+           "parse_streams", "Decoder", "HJOB_DTYPE", "scan_streams", "huffman_execute", "decode_streams"]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 
@@ -28,7 +28,13 @@ GRANULE_DTYPE = np.dtype([("header", "<u4"), ("gr", "<u4"), ("ch", CHANNEL_DTYPE
                           ("reserved", "u1", (8,))])
 STREAM_DTYPE = np.dtype([("first_granule", "<u8"), ("n_granules", "<u4"), ("flags", "<u4")])
 STATE_DTYPE = np.dtype([("store", "<f4", (2, 32, 18)), ("vvec", "<f4", (2, 1024))])
-assert CHANNEL_DTYPE.itemsize == 72 and GRANULE_DTYPE.itemsize == 160
+# one Huffman job per (granule, channel) of the GPU main-data path (mp3g_hjob)
+HJOB_DTYPE = np.dtype([("part2_start", "<u8"), ("bit_end", "<u8"), ("scf0_delta", "<u4"),
+                       ("part2_3_length", "<u2"), ("big_values", "<u2"), ("region1_start", "<u2"),
+                       ("region2_start", "<u2"), ("table_select", "u1", (3,)), ("count1_table", "u1"),
+                       ("sf_kind", "u1"), ("scfsi", "u1"), ("slen", "u1", (4,)), ("nsf", "u1", (4,)),
+                       ("sf0_kind", "u1"), ("sf0_slen", "u1", (2,)), ("reserved", "u1", (3,))])
+assert CHANNEL_DTYPE.itemsize == 72 and GRANULE_DTYPE.itemsize == 160 and HJOB_DTYPE.itemsize == 48
 assert STREAM_DTYPE.itemsize == 16 and STATE_DTYPE.itemsize == 12800
 
 MODE_EXACT, MODE_FAST, FLAG_CHECKED, FLAG_KERNEL_V1 = 0, 1, 0x100, 0x200
@@ -77,6 +83,12 @@ def lib():
         L.mp3g_parse_streams.argtypes = [u32, vp, vp, C.c_int, C.POINTER(vp), C.POINTER(vp),
                                          C.POINTER(u64), vp, vp]
         L.mp3g_free.argtypes = [vp]
+        L.mp3g_scan_streams.argtypes = [u32, vp, vp, C.c_int, C.POINTER(vp)]
+        L.mp3g_scan_buffers.argtypes = [vp, C.POINTER(u64), C.POINTER(u64)] + [C.POINTER(vp)] * 5
+        L.mp3g_scan_free.argtypes = [vp]
+        L.mp3g_huffman_execute.argtypes = [C.c_int, vp, u64, vp, vp, vp, vp]
+        L.mp3g_decode_streams.argtypes = [C.c_int, u32, vp, vp, C.c_int, u32, C.POINTER(vp), C.POINTER(u64),
+                                          vp, vp]
         L.mp3g_decoder_new.argtypes = [vp, sz, C.c_int, C.c_int, u32, C.POINTER(vp)]
         L.mp3g_decoder_free.argtypes = [vp]
         L.mp3g_decoder_read.argtypes = [vp, vp, sz, C.POINTER(sz)]
@@ -185,6 +197,65 @@ def parse_streams(datas, n_threads=0):
     k = n.value
     return (_take(g, k, GRANULE_DTYPE, (k,)), _take(c, k, np.int16, (k, 2, 576)), streams,
             status[:len(datas)])
+
+
+def _copy_out(ptr, nbytes, dtype):
+    if nbytes == 0:
+        return np.zeros(0, dtype)
+    raw = np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_uint8)), shape=(nbytes,))
+    return raw.view(dtype).copy()
+
+
+def _stream_args(datas):
+    bufs = [np.frombuffer(d, dtype=np.uint8) if len(d) else np.zeros(1, np.uint8) for d in datas]
+    ptrs = (C.c_void_p * max(1, len(bufs)))(*[b.ctypes.data for b in bufs])
+    lens = (C.c_size_t * max(1, len(bufs)))(*[len(d) for d in datas])
+    return bufs, ptrs, lens
+
+
+def scan_streams(datas, n_threads=0):
+    """Host scan of the GPU main-data path (mp3g_scan_streams).
+
+    Returns numpy copies: granules (side-info fields set), jobs [HJOB_DTYPE]
+    (two per granule), main_data (uint8, padded), streams, end_status."""
+    bufs, ptrs, lens = _stream_args(datas)
+    h = C.c_void_p()
+    _check(lib().mp3g_scan_streams(len(datas), ptrs, lens, n_threads, C.byref(h)))
+    try:
+        ng, nmd = C.c_uint64(), C.c_uint64()
+        pg, pj, pm, ps, pst = (C.c_void_p() for _ in range(5))
+        _check(lib().mp3g_scan_buffers(h, C.byref(ng), C.byref(nmd), C.byref(pg), C.byref(pj), C.byref(pm),
+                                       C.byref(ps), C.byref(pst)))
+        n = ng.value
+        return {"granules": _copy_out(pg, n * GRANULE_DTYPE.itemsize, GRANULE_DTYPE),
+                "jobs": _copy_out(pj, 2 * n * HJOB_DTYPE.itemsize, HJOB_DTYPE),
+                "main_data": _copy_out(pm, nmd.value, np.uint8),
+                "streams": _copy_out(ps, len(datas) * STREAM_DTYPE.itemsize, STREAM_DTYPE),
+                "end_status": _copy_out(pst, len(datas) * 4, np.int32)}
+    finally:
+        lib().mp3g_scan_free(h)
+
+
+def huffman_execute(d_jobs, n_granules, d_main_data, d_granules, d_coeffs, stream=None, device=0):
+    """Device scale-factor + Huffman decode of 2 * n_granules jobs (mp3g_huffman_execute);
+    buffers are device pointers (ints) or torch tensors, stream a hipStream_t int."""
+    def p(x):
+        return C.c_void_p(x.data_ptr() if hasattr(x, "data_ptr") else int(x))
+    _check(lib().mp3g_huffman_execute(device, p(d_jobs), n_granules, p(d_main_data), p(d_granules),
+                                      p(d_coeffs), C.c_void_p(stream) if stream else None))
+
+
+def decode_streams(datas, mode=MODE_EXACT, n_threads=0, device=0):
+    """Bitstreams in, PCM out on the GPU (mp3g_decode_streams): scan on the host,
+    Huffman + DSP on the device.  Returns (pcm int16[n, 576, 2], streams, end_status)."""
+    bufs, ptrs, lens = _stream_args(datas)
+    streams = np.zeros(len(datas), STREAM_DTYPE)
+    status = np.zeros(max(1, len(datas)), np.int32)
+    pcm, n = C.c_void_p(), C.c_uint64()
+    _check(lib().mp3g_decode_streams(device, len(datas), ptrs, lens, n_threads, mode, C.byref(pcm), C.byref(n),
+                                     _ptr(streams), _ptr(status)))
+    k = n.value
+    return _take(pcm, k, np.int16, (k, 576, 2)), streams, status[:len(datas)]
 
 
 class Decoder:

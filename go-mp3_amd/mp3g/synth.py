@@ -12,7 +12,14 @@ reference's bitstream parse guarantees:
   * no MPEG-2 mixed blocks (the reference panics on them, maindata.go:139-178).
 
 Everything is deterministic in (seed, shape).
+
+encode_stream() goes one step further and writes real Layer III BITSTREAMS
+(synthetic writer go-mp3_amd/csrc/synth_enc.cpp, libmp3gsynth.so) for the
+bitstream workloads of the GPU main-data path.
 """
+import ctypes as C
+import os
+
 import numpy as np
 
 from . import GRANULE_DTYPE, streams_for
@@ -188,3 +195,46 @@ def synth_pool_batch(n_streams, n_frames, seed=1, pool_frames=4096, **kw):
     starts = rng.integers(0, npg // 2, n_streams) * 2  # frame-aligned rotation
     idx = (starts[:, None] + np.arange(per)[None, :]) % npg
     return pg, pc, idx.reshape(-1), streams_for([per] * n_streams)
+
+
+# ---- synthetic bitstreams (libmp3gsynth.so, tooling) --------------------------
+class _SynthParams(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("n_frames", C.c_int32), ("lsf", C.c_int32), ("mode", C.c_int32),
+                ("bitrate_index", C.c_int32), ("sfreq", C.c_int32), ("pad_", C.c_int32),
+                ("p_ms", C.c_double), ("p_is", C.c_double), ("p_event", C.c_double), ("p_mixed", C.c_double),
+                ("p_big", C.c_double), ("fill", C.c_double)]
+
+
+_synth_lib = None
+
+
+def _synth():
+    global _synth_lib
+    if _synth_lib is None:
+        L = C.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmp3gsynth.so"))
+        L.mp3g_synth_encode.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p]
+        L.mp3g_synth_encode.restype = C.c_int64
+        _synth_lib = L
+    return _synth_lib
+
+
+def encode_stream(seed, n_frames, mode=MODE_JOINT, lsf=False, bitrate_index=None, sfreq=0, p_ms=0.5, p_is=0.1,
+                  p_event=0.03, p_mixed=0.01, p_big=0.002, fill=0.9, expected=False):
+    """A seeded Layer III bitstream: CBR frames (128 kbps MPEG-1 / 64 kbps MPEG-2
+    by default) through the bit reservoir.  With expected=True also returns the
+    granule descriptors + coefficients a decoder must recover from it."""
+    if bitrate_index is None:
+        bitrate_index = 8 if lsf else 9
+    p = _SynthParams(seed, n_frames, int(lsf), mode, bitrate_index, sfreq, 0, p_ms, p_is, p_event, p_mixed,
+                     p_big, fill)
+    cap = n_frames * 1500 + 64
+    out = np.zeros(cap, np.uint8)
+    ng = n_frames * (1 if lsf else 2)
+    g = np.zeros(ng, GRANULE_DTYPE) if expected else None
+    c = np.zeros((ng, 2, 576), np.int16) if expected else None
+    n = _synth().mp3g_synth_encode(C.byref(p), out.ctypes.data, cap, None if g is None else g.ctypes.data,
+                                   None if c is None else c.ctypes.data)
+    if n <= 0:
+        raise RuntimeError("mp3g_synth_encode failed")
+    data = out[:n].tobytes()
+    return (data, g, c) if expected else data

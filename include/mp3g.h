@@ -183,6 +183,82 @@ int mp3g_parse_streams(uint32_t n_streams, const uint8_t* const* datas, const si
                        int* end_status);
 void mp3g_free(void* p);
 
+/* ---- main-data decode on the GPU --------------------
+ * Splits frame.Read (frame.go:67-115) at the bit reservoir:
+ *   host   (mp3g_scan_streams): tags, sync search, header, side info and the
+ *          reservoir resolution -- sequential but byte-level, no Huffman;
+ *   device (mp3g_huffman_execute): scale factors (maindata.go:119-288) and
+ *          Huffman decoding (maindata/huffman.go:27-138, huffman/huffman.go:
+ *          348-419) of every (granule, channel) in parallel, completing the
+ *          granule descriptors and writing the int16 coefficients that
+ *          mp3g_plan_execute consumes.
+ * The result is byte-identical to mp3g_parse_streams.  The main data of each
+ * stream is concatenated into one byte buffer; frame f's bit buffer (the
+ * reference's `prev.Tail(main_data_begin) ++ buf`, or `prev ++ buf` on a
+ * reservoir underflow, maindata.go:290-323) is always a suffix of that
+ * concatenation ending at bit_end, so jobs address it with absolute bit
+ * positions.
+ *
+ * One job per (granule, channel), jobs[2*g + ch]; 48 bytes. */
+#define MP3G_SF_NONE 0        /* channel absent (mono): zero coefficients      */
+#define MP3G_SF_MPEG1_LONG 1  /* maindata.go:233-279 (scfsi copies from gr 0) */
+#define MP3G_SF_MPEG1_SHORT 2 /* maindata.go:221-231                          */
+#define MP3G_SF_MPEG1_MIXED 3 /* maindata.go:207-220                          */
+#define MP3G_SF_MPEG2_LONG 4  /* maindata.go:132-172, 22 scale factors        */
+#define MP3G_SF_MPEG2_SHORT 5 /* maindata.go:173-179, 39 scale factors        */
+typedef struct mp3g_hjob {
+  uint64_t part2_start;     /* absolute bit position of the scale factors (maindata.go:202) */
+  uint64_t bit_end;         /* end of the frame's main-data bits: reads at/after it yield 0
+                               and do not advance (bits.go:45-77) */
+  uint32_t scf0_delta;      /* MPEG-1 granule 1 with scfsi: granule 0's part2_start is
+                               part2_start - scf0_delta */
+  uint16_t part2_3_length;  /* sideinfo.go:114 */
+  uint16_t big_values;      /* <= 288 (more is a frame error, found by the scan) */
+  uint16_t region1_start;   /* lines (maindata/huffman.go:39-64) */
+  uint16_t region2_start;
+  uint8_t table_select[3];
+  uint8_t count1_table;     /* count1table_select */
+  uint8_t sf_kind;          /* MP3G_SF_* */
+  uint8_t scfsi;            /* granule 1: bit k = scale-factor part k copied from granule 0 */
+  uint8_t slen[4];          /* bits per scale factor: MPEG-1 {slen1, slen2}; MPEG-2 per part */
+  uint8_t nsf[4];           /* MPEG-2: scale factors per part (ISO 13818-3 Table 6) */
+  uint8_t sf0_kind;         /* granule 0's sf_kind and slen (for the scfsi copy) */
+  uint8_t sf0_slen[2];
+  uint8_t reserved[3];
+} mp3g_hjob;
+
+/* Host scan of many streams on n_threads host threads (0 = all cores).  The
+ * scan owns its buffers until mp3g_scan_free; mp3g_scan_buffers returns:
+ *   granules   [n_granules] descriptors with the side-info fields set (scale
+ *              factors and count1 are written by mp3g_huffman_execute)
+ *   jobs       [2 * n_granules]
+ *   main_data  [main_data_bytes] (incl. 16 zero bytes of padding)
+ *   streams    [n_streams] where each stream's granules landed
+ *   end_status [n_streams] as mp3g_parse_streams.
+ * A frame the reference rejects (frame.Read error or panic) ends its stream
+ * exactly where mp3g_parse_streams ends it. */
+typedef struct mp3g_scan mp3g_scan;
+int mp3g_scan_streams(uint32_t n_streams, const uint8_t* const* datas, const size_t* lens, int n_threads,
+                      mp3g_scan** out);
+int mp3g_scan_buffers(const mp3g_scan* scan, uint64_t* n_granules, uint64_t* main_data_bytes,
+                      const mp3g_granule** granules, const mp3g_hjob** jobs, const uint8_t** main_data,
+                      const mp3g_stream** streams, const int** end_status);
+void mp3g_scan_free(mp3g_scan* scan);
+
+/* Device decode of the 2 * n_granules jobs (device pointers; d_granules holds
+ * the scan's descriptors and is completed in place).  Asynchronous on
+ * hip_stream (NULL = default stream). */
+int mp3g_huffman_execute(int device, const mp3g_hjob* d_jobs, uint64_t n_granules, const uint8_t* d_main_data,
+                         mp3g_granule* d_granules, int16_t* d_coeffs, void* hip_stream);
+
+/* Bitstreams in, PCM out (the batch drop-in): scan on the host, Huffman + DSP
+ * on `device`.  *pcm (library-allocated, free with mp3g_free) holds
+ * n_granules blocks of 576 stereo s16 samples; streams / end_status as
+ * mp3g_parse_streams. */
+int mp3g_decode_streams(int device, uint32_t n_streams, const uint8_t* const* datas, const size_t* lens,
+                        int n_threads, uint32_t mode, int16_t** pcm, uint64_t* n_granules,
+                        mp3g_stream* streams, int* end_status);
+
 /* ---- decoder: mp3.NewDecoder / io.Reader / io.Seeker (decode.go:27-388) ----
  * Parses on the host with read-ahead and decodes batches of frames on
  * `device` (mode = MP3G_MODE_EXACT | MP3G_MODE_FAST).  `data` is copied.

@@ -42,6 +42,9 @@ def test_struct_layouts_match_c(tmp_path):
         "mp3g_granule": ["header", "gr", "ch", "reserved"],
         "mp3g_stream": ["first_granule", "n_granules", "flags"],
         "mp3g_state": ["store", "vvec"],
+        "mp3g_hjob": ["part2_start", "bit_end", "scf0_delta", "part2_3_length", "big_values", "region1_start",
+                      "region2_start", "table_select", "count1_table", "sf_kind", "scfsi", "slen", "nsf",
+                      "sf0_kind", "sf0_slen", "reserved"],
     }
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void){"]
     for st, fs in fields.items():
@@ -60,7 +63,11 @@ def test_struct_layouts_match_c(tmp_path):
            "mp3g_stream": mp3g.STREAM_DTYPE, "mp3g_state": mp3g.STATE_DTYPE}
     odts = {"mp3g_channel": oracle.CHANNEL_DTYPE, "mp3g_granule": oracle.GRANULE_DTYPE,
             "mp3g_stream": oracle.STREAM_DTYPE, "mp3g_state": oracle.STATE_DTYPE}
-    for st, fs in fields.items():
+    assert c_layout[("mp3g_hjob", "size")] == mp3g.HJOB_DTYPE.itemsize
+    for f in fields["mp3g_hjob"]:
+        assert c_layout[("mp3g_hjob", f)] == mp3g.HJOB_DTYPE.fields[f][1], f
+    for st in ("mp3g_channel", "mp3g_granule", "mp3g_stream", "mp3g_state"):
+        fs = fields[st]
         assert c_layout[(st, "size")] == dts[st].itemsize == odts[st].itemsize
         for f in fs:
             assert c_layout[(st, f)] == dts[st].fields[f][1] == odts[st].fields[f][1], (st, f)

@@ -1,0 +1,124 @@
+"""Main-data decode on the GPU (huffman_dev.hip) against
+the host parse, and the whole bitstream path against the oracle.
+
+The host scan (mp3g_scan_streams) resolves headers, side info and the bit
+reservoir; the device decodes scale factors + Huffman codes of every
+(granule, channel) in parallel.  The bar is byte equality with the product's
+host parse (mp3g_parse_streams, itself byte-identical to the oracle:
+test_parse_cpu.py) -- every granule descriptor, every coefficient, the same
+stream lengths and end statuses -- on the sample streams, the reference's
+fuzz corpus, trailing-tag constructions, 120 seeded mutations (truncations,
+bit flips, overwritten runs, splices: reservoir underflows, reads past the
+end of the main data, count1 overruns) and synthetic bitstreams (mixed
+blocks, intensity stereo, linbits tables, MPEG-2, a full reservoir).  Then
+mp3g_decode_streams (scan + device Huffman + device DSP) against the
+oracle's PCM: bit-exact in exact mode, +-1 LSB in fast mode.
+"""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from test_oracle_kats import GOLDEN, ape_tag, id3v1, minimal_frame
+from test_parse_cpu import mutations
+from test_scan_cpu import WRITER_CASES
+
+pytestmark = pytest.mark.gpu
+
+
+def gpu_parse(gpu, datas):
+    """scan on the host, Huffman on cuda:0 -> (granules, coeffs, streams, end_status)."""
+    import torch
+    dev = torch.device("cuda:0")
+    s = gpu.scan_streams(datas, n_threads=4)
+    n = len(s["granules"])
+    if n == 0:
+        return s["granules"], np.zeros((0, 2, 576), np.int16), s["streams"], s["end_status"]
+    d_g = torch.from_numpy(s["granules"].view(np.uint8).copy()).to(dev)
+    d_j = torch.from_numpy(s["jobs"].view(np.uint8).copy()).to(dev)
+    d_m = torch.from_numpy(s["main_data"].copy()).to(dev)
+    d_c = torch.full((n * 1152,), 0x5A5A, dtype=torch.int16, device=dev)  # poison: every line must be written
+    gpu.huffman_execute(d_j, n, d_m, d_g, d_c, stream=torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize(dev)
+    g = d_g.cpu().numpy().view(gpu.GRANULE_DTYPE)
+    c = d_c.cpu().numpy().reshape(n, 2, 576)
+    return g, c, s["streams"], s["end_status"]
+
+
+def assert_same_as_host(gpu, datas, what):
+    g, c, s, st = gpu_parse(gpu, datas)
+    g2, c2, s2, st2 = gpu.parse_streams(datas, n_threads=4)
+    assert np.array_equal(st, st2), (what, st, st2)
+    assert np.array_equal(s, s2), what
+    assert len(g) == len(g2), what
+    if len(g):
+        bad = np.nonzero((g.view(np.uint8).reshape(len(g), -1) != g2.view(np.uint8).reshape(len(g2), -1)).any(1))[0]
+        assert len(bad) == 0, f"{what}: descriptors differ at granules {bad[:10]}"
+        badc = np.nonzero((c != c2).any(axis=(1, 2)))[0]
+        assert len(badc) == 0, f"{what}: coefficients differ at granules {badc[:10]}"
+    return g, c
+
+
+@pytest.mark.parametrize("name", ["classic_lame.mp3", "mpeg2.mp3"])
+def test_sample_files(gpu, sample_files, golden, name):
+    g, c = assert_same_as_host(gpu, [sample_files[name]], name)
+    assert hashlib.sha256(g.tobytes()).hexdigest() == golden["files"][name]["descriptor_sha256"]
+    assert hashlib.sha256(c.tobytes()).hexdigest() == golden["files"][name]["coeff_sha256"]
+
+
+def test_fuzz_corpus_and_tags(gpu):
+    d = os.path.join(GOLDEN, "fuzz")
+    datas = [open(os.path.join(d, f), "rb").read() for f in sorted(os.listdir(d))]
+    tails = [b"", ape_tag(), id3v1(), ape_tag() + id3v1(),
+             bytes(np.random.default_rng(1).integers(0, 255, 100 * 1024, dtype=np.uint8) & 0x7F)]
+    datas += [minimal_frame() * 10 + t for t in tails]
+    datas += [b"", b"\xff", b"ID3", minimal_frame() * 2 + bytes(70 * 1024)]
+    assert_same_as_host(gpu, datas, "fuzz corpus + tags")
+
+
+@pytest.mark.parametrize("name", ["classic_lame.mp3", "mpeg2.mp3"])
+def test_differential_mutations(gpu, sample_files, name):
+    rng = np.random.default_rng(77 + len(name))
+    assert_same_as_host(gpu, mutations(sample_files[name][:60000], rng, 60), f"{name} mutations")
+
+
+def test_synthetic_bitstreams(gpu):
+    from mp3g import synth
+    datas = [synth.encode_stream(k, 200, **kw) for k, kw in enumerate(WRITER_CASES.values())]
+    datas += mutations(datas[1], np.random.default_rng(5), 20)
+    g, c = assert_same_as_host(gpu, datas, "synthetic")
+    assert (g["ch"]["mixed_block_flag"] == 1).any() and (g["ch"]["block_type"] == 2).any()
+
+
+def test_large_batch(gpu):
+    """Many streams in one launch (several thousand workgroups)."""
+    from mp3g import synth
+    datas = [synth.encode_stream(100 + k, 64, p_event=0.05, p_mixed=0.05) for k in range(256)]
+    assert_same_as_host(gpu, datas, "256 streams")
+
+
+def test_bitstream_path_pcm(gpu, sample_files, golden):
+    """scan + device Huffman + device DSP (mp3g_decode_streams) vs the oracle."""
+    names = ["classic_lame.mp3", "mpeg2.mp3"]
+    datas = [sample_files[n] for n in names]
+    pcm, streams, st = gpu.decode_streams(datas, mode=gpu.MODE_EXACT)
+    assert list(st) == [7, 7]
+    for k, n in enumerate(names):
+        lo, m = int(streams[k]["first_granule"]), int(streams[k]["n_granules"])
+        assert hashlib.sha256(pcm[lo:lo + m].tobytes()).hexdigest() == golden["files"][n]["pcm_sha256"], n
+    pcm_f, _, _ = gpu.decode_streams(datas, mode=gpu.MODE_FAST)
+    assert np.abs(pcm_f.astype(np.int32) - pcm).max() <= 1
+
+
+def test_bitstream_path_synthetic_vs_oracle(gpu):
+    from mp3g import synth
+    datas = [synth.encode_stream(11 + k, 120, p_mixed=0.2, p_event=0.1, p_is=0.4) for k in range(6)]
+    datas.append(synth.encode_stream(99, 120, lsf=True, p_event=0.1))
+    pcm, streams, st = gpu.decode_streams(datas, mode=gpu.MODE_EXACT)
+    for k, d in enumerate(datas):
+        ost, opcm = oracle.decode_all(d)
+        lo, m = int(streams[k]["first_granule"]), int(streams[k]["n_granules"])
+        assert ost == oracle.ORC_OK and st[k] == 7
+        assert pcm[lo:lo + m].tobytes() == opcm, k

@@ -1,0 +1,129 @@
+"""GPU main-data path, host side, checked on the CPU.
+
+* The synthetic bitstream writer (tooling, go-mp3_amd/csrc/synth_enc.cpp):
+  every stream decodes -- through the oracle AND through the product's host
+  parse -- to exactly the descriptors and coefficients the writer intended
+  (an independent check of both parses: mixed blocks, scfsi, linbits tables,
+  MPEG-2 scale-factor layouts, the bit reservoir at its 511-byte limit).
+* The host scan (mp3g_scan_streams): same stream table, end statuses and
+  side-info fields as the host parse.
+* The job decomposition: the device's per-job decoder (huffman_job.h,
+  __host__ __device__) compiled for the CPU by tests/native/hjob_host.hip
+  (test infrastructure) reproduces the host parse byte for byte from the
+  scan's jobs and main-data buffer -- on the sample streams, the fuzz corpus,
+  120 seeded mutations and synthetic streams.  The GPU run of the same code
+  is tests/test_gpu_huffman.py.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import mp3g
+import oracle
+from mp3g import synth
+from test_oracle_kats import GOLDEN
+from test_parse_cpu import mutations
+
+from conftest import REPO
+
+WRITER_CASES = {
+    "joint": dict(),
+    "mixed+is": dict(p_mixed=0.3, p_event=0.1, p_is=0.5),
+    "mono+linbits": dict(mode=synth.MODE_MONO, p_big=0.02),
+    "mpeg2": dict(lsf=True, p_event=0.1),
+    "mpeg2-mono": dict(lsf=True, mode=synth.MODE_MONO),
+    "reservoir-full": dict(fill=1.3),
+    "stereo": dict(mode=synth.MODE_STEREO),
+    "dual": dict(mode=synth.MODE_DUAL),
+    "48k": dict(sfreq=1, bitrate_index=10),
+    "32k-320": dict(sfreq=2, bitrate_index=14, p_big=0.01),
+}
+
+
+@pytest.mark.parametrize("case", sorted(WRITER_CASES))
+def test_writer_roundtrip(case):
+    data, g, c = synth.encode_stream(3, 120, expected=True, **WRITER_CASES[case])
+    st, _, g2, c2 = oracle.decode_all_capture(data)
+    assert st == oracle.ORC_OK and len(g2) == len(g)
+    assert g2.tobytes() == g.tobytes(), case
+    assert np.array_equal(c2, c), case
+    g3, c3, end = mp3g.parse_stream(data)
+    assert end == 7 and g3.tobytes() == g.tobytes() and np.array_equal(c3, c), case
+
+
+def test_writer_uses_the_reservoir_and_cbr_sizes():
+    data = synth.encode_stream(1, 200, fill=1.1)
+    b = np.frombuffer(data, np.uint8)
+    off, mdb, n = 0, [], 0
+    while off < len(b):
+        h = int.from_bytes(b[off:off + 4].tobytes(), "big")
+        assert h >> 21 == 0x7FF
+        mdb.append((int(b[off + 4]) << 1) | (int(b[off + 5]) >> 7))
+        off += 144 * 128000 // 44100 + ((h >> 9) & 1)
+        n += 1
+    assert off == len(b) and n == 200
+    assert mdb[0] == 0 and max(mdb) > 300 and np.mean(np.array(mdb) > 0) > 0.9
+
+
+def _masked(g):
+    g = g.copy()
+    g["ch"]["count1"] = 0
+    g["ch"]["scalefac_l"] = 0
+    g["ch"]["scalefac_s"] = 0
+    return g
+
+
+@pytest.fixture(scope="module")
+def hjob_host(tmp_path_factory):
+    """tests/native/hjob_host.hip: the device job decoder built for the CPU."""
+    out = tmp_path_factory.mktemp("native") / "libhjob_host.so"
+    subprocess.check_call(["/opt/rocm/bin/hipcc", "-O2", "-std=c++17", "-fPIC", "-shared", "--offload-arch=gfx950",
+                           "-o", str(out), os.path.join(REPO, "tests", "native", "hjob_host.hip"),
+                           os.path.join(REPO, "go-mp3_amd", "csrc", "huff_lut.cpp")])
+    L = C.CDLL(str(out))
+    L.hjob_decode_host.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p]
+    return L
+
+
+def check_against_parse(hjob_host, datas, what):
+    s = mp3g.scan_streams(datas, n_threads=4)
+    g2, c2, s2, st2 = mp3g.parse_streams(datas, n_threads=4)
+    assert np.array_equal(s["end_status"], st2), (what, s["end_status"], st2)
+    assert np.array_equal(s["streams"], s2), what
+    assert _masked(s["granules"]).tobytes() == _masked(g2).tobytes(), what
+    n = len(g2)
+    jobs = s["jobs"]
+    assert ((jobs["sf_kind"][1::2] == 0) == (((s["granules"]["header"] >> 6) & 3) == 3)).all()
+    assert (jobs["big_values"][jobs["part2_3_length"] > 0] <= 288).all()
+    g = s["granules"].copy()
+    c = np.full((n, 2, 576), 0x5A5A, np.int16)  # poison: every line must be written
+    assert hjob_host.hjob_decode_host(jobs.ctypes.data, n, s["main_data"].ctypes.data, g.ctypes.data,
+                                      c.ctypes.data) == 0
+    assert g.tobytes() == g2.tobytes(), f"{what}: descriptors differ"
+    assert np.array_equal(c, c2), f"{what}: coefficients differ"
+
+
+def test_jobs_sample_files(hjob_host, sample_files):
+    check_against_parse(hjob_host, list(sample_files.values()), "sample files")
+
+
+def test_jobs_fuzz_corpus(hjob_host):
+    d = os.path.join(GOLDEN, "fuzz")
+    check_against_parse(hjob_host, [open(os.path.join(d, f), "rb").read() for f in sorted(os.listdir(d))], "fuzz")
+
+
+@pytest.mark.parametrize("name", ["classic_lame.mp3", "mpeg2.mp3"])
+def test_jobs_mutations(hjob_host, sample_files, name):
+    rng = np.random.default_rng(77 + len(name))
+    check_against_parse(hjob_host, mutations(sample_files[name][:60000], rng, 60), f"{name} mutations")
+
+
+def test_jobs_synthetic(hjob_host):
+    datas = [synth.encode_stream(k, 150, **kw) for k, kw in enumerate(WRITER_CASES.values())]
+    # corrupt copies: truncated mid-reservoir, flipped side-info bits
+    rng = np.random.default_rng(5)
+    datas += mutations(datas[1], rng, 20)
+    check_against_parse(hjob_host, datas, "synthetic")
