@@ -67,6 +67,10 @@ struct __align__(16) SharedSmem {
   float isr[8][2];
   float dct[32][16];   // FastTables::dct rows (one row per lane, read once per granule)
   float dwin[32][16];  // FastTables::dwin rows, pre-scaled by 32767
+  // FastTables::lband: read per lane every granule, so it lives in LDS -- a
+  // vector global load there would wait (vmcnt is in order) for the previous
+  // granule's PCM stores
+  uint32_t lband[kCombos][32];
 };
 // per-wave working set ~11.9 KB.  The workgroup (4 waves + shared tables) must
 // stay <= 42 x 1280 B (gfx950 LDS allocation granule) for 3 workgroups
@@ -75,7 +79,6 @@ struct __align__(16) WaveSmem {
   union {
     int16_t raw[2][576];  // Huffman integers of the current granule
     f2 eo[2][3][32];      // folded matrixing input of 6 slots [ch][slot pair][k]: even k<16, odd 16+k
-    int16_t pcm[576 * 2]; // s16 stereo output staged for 16-B stores
   } a;
   float ring[2][kRing][32];
   // requantization exponents n4 of the long bands [ch][sfb] and short bands [ch][sfb][win]
@@ -221,6 +224,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       (&sh.dct[0][0])[e] = (&g_fast.dct[0][0])[e];
       (&sh.dwin[0][0])[e] = (&g_fast.dwin[0][0])[e] * 32767.0f;
     }
+    for (int e = t; e < kCombos * 32; e += kLanes * kWaves) (&sh.lband[0][0])[e] = (&g_fast.lband[0][0])[e];
   }
   __syncthreads();  // the only workgroup barrier: the waves are independent from here on
   const int lane = threadIdx.x & (kLanes - 1);
@@ -242,6 +246,12 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
   const uint32_t out_first = __builtin_amdgcn_readfirstlane((uint32_t)cd.out_first);
   const uint32_t end = __builtin_amdgcn_readfirstlane((uint32_t)(cd.out_first + cd.n_out));
   const mp3g_state* sin = state_in ? state_in + cd.stream : nullptr;
+  // this chunk's descriptors as a buffer resource (SGPRs): the next granule's
+  // descriptor is prefetched through an SGPR base and 32-bit offsets, so no
+  // 64-bit pointer is kept (and spilled) in VGPRs -- a spill reload costs an
+  // s_waitcnt vmcnt(0), which would also wait for the coefficient prefetch
+  const __amdgpu_buffer_rsrc_t rs_desc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<mp3g_granule*>(gran + w), (short)0, (int)((end - w) * sizeof(mp3g_granule)), 0x00020000);
 
   // entry state: overlap store in registers, V history as X vectors
   float st[18];
@@ -267,7 +277,8 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     // does a replayed granule's V feed anything? (see v2 / DESIGN.md halo)
     bool need_v = true;
     if (!out && g + 1 < out_first) need_v = hdr_nch(gran[g + 1].header) < hdr_nch(s.desc.header);
-    const uint32_t h = s.desc.header;
+    // wave-uniform (SGPR): the per-combo tables below become scalar loads
+    const uint32_t h = __builtin_amdgcn_readfirstlane(s.desc.header);
     const int nch = hdr_nch(h), combo = hdr_combo(h);
     const bool act = ch < nch;
     // lanes of an absent channel mirror channel 0's block layout (no extra divergence)
@@ -319,7 +330,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
         xi[2 * q + 1] = (int)(int16_t)(w >> 16);
       }
       // long band of line j: first band of the subband + band starts among lines 1..j
-      const uint32_t lb = g_fast.lband[combo][k];
+      const uint32_t lb = sh.lband[combo][k];
       int ex[18];
 #pragma unroll
       for (int j = 0; j < 18; j++)
@@ -493,7 +504,10 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       p0 = src[lane];
       p1 = src[lane + 64];
       if (lane < 16) p2 = src[lane + 128];
-      if (lane < 10) pd = reinterpret_cast<const uint4*>(gran + g + 1)[lane];
+      if (lane < 10) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs_desc, lane * 16, (int)((g + 1 - w) * sizeof(mp3g_granule)), 0);
+        pd = make_uint4(v[0], v[1], v[2], v[3]);
+      }
     }
 
     // ---- matrixing, in two halves of 9 time slots: even/odd fold of S across
@@ -536,8 +550,22 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       if (third) stamp(3 + third);
     }
 
-    // ---- 16-tap window over the X ring -> s16 PCM ----
-    if (out && act) {
+    // ---- next granule in: raw/eo (dead after the matrixing) and the
+    //      descriptor (not read again this granule) take the prefetch now,
+    //      before the PCM stores are issued -- vmcnt counts loads and stores in
+    //      issue order, so a wait for the prefetch after the stores would wait
+    //      for the stores too ----
+    if (more) {
+      uint4* dst = reinterpret_cast<uint4*>(&s.a.raw[0][0]);
+      dst[lane] = p0;
+      dst[lane + 64] = p1;
+      if (lane < 16) dst[lane + 128] = p2;
+      if (lane < 10) reinterpret_cast<uint4*>(&s.desc)[lane] = pd;
+    }
+
+    // ---- 16-tap window over the X ring -> s16 PCM, stored straight to HBM ----
+    // (lanes of an absent channel compute values that are never stored)
+    if (out) {
       float dw[16];
       {
         const float4* d4 = reinterpret_cast<const float4*>(&sh.dwin[k][0]);
@@ -572,38 +600,33 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
 #pragma unroll
         for (int i = 0; i < 9; i++) acc[9 * pass + i] = acc2[i].x + acc2[i].y;
       }
-      // s16 into the LDS staging area (raw/eo are dead until the next granule
-      // is written in), then 16-B coalesced stores
-      int16_t* P = s.a.pcm;
+      // (L, R) sample pairs without LDS staging: one v_permlane32_swap per slot
+      // pair hands lane i slot 2p's (L, R) and lane 32 + i slot 2p + 1's, so
+      // every lane stores one dword per slot pair and the wave 2 x 128
+      // contiguous bytes.  Mono: both halves of the dword are the channel
+      // (frame.go:671-678).
+      uint32_t* P = reinterpret_cast<uint32_t*>(pcm + (size_t)g * 1152);
+      const int hi = lane >> 5;
 #pragma unroll
-      for (int ss = 0; ss < 18; ss++) {
-        const int16_t v = (int16_t)(int)__builtin_amdgcn_fmed3f(acc[ss], -32767.0f, 32767.0f);
-        P[2 * (32 * ss + k) + ch] = v;
-        if (nch == 1) P[2 * (32 * ss + k) + 1] = v;  // mono: both slots (frame.go:671-678)
+      for (int p = 0; p < 9; p++) {
+        const int a = (int)__builtin_amdgcn_fmed3f(acc[2 * p], -32767.0f, 32767.0f);
+        const int b = (int)__builtin_amdgcn_fmed3f(acc[2 * p + 1], -32767.0f, 32767.0f);
+        if (nch == 2) {
+          const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+          P[32 * (2 * p + hi) + k] = ((uint32_t)r[0] & 0xffffu) | ((uint32_t)r[1] << 16);
+        } else if (!hi) {
+          P[32 * (2 * p) + k] = ((uint32_t)a & 0xffffu) | ((uint32_t)a << 16);
+          P[32 * (2 * p + 1) + k] = ((uint32_t)b & 0xffffu) | ((uint32_t)b << 16);
+        }
       }
     }
-    if (out) {
-      wave_sync();
-      const uint4* src = reinterpret_cast<const uint4*>(s.a.pcm);
-      uint4* dst = reinterpret_cast<uint4*>(pcm + (size_t)g * 1152);
-      dst[lane] = src[lane];
-      dst[lane + 64] = src[lane + 64];
-      if (lane < 16) dst[lane + 128] = src[lane + 128];
-    }
-    wave_sync();  // ring reads done, staging area free
+    wave_sync();  // ring reads done
     stamp(6);
 
-    // ---- history shift (channels this granule touched) + next granule in ----
+    // ---- history shift (channels this granule touched) ----
     for (int e = lane; e < nch * (kHist * 8); e += kLanes) {
       const int c = e / (kHist * 8), r4 = e % (kHist * 8);
       reinterpret_cast<float4*>(&s.ring[c][0][0])[r4] = reinterpret_cast<const float4*>(&s.ring[c][18][0])[r4];
-    }
-    if (more) {
-      uint4* dst = reinterpret_cast<uint4*>(&s.a.raw[0][0]);
-      dst[lane] = p0;
-      dst[lane + 64] = p1;
-      if (lane < 16) dst[lane + 128] = p2;
-      if (lane < 10) reinterpret_cast<uint4*>(&s.desc)[lane] = pd;
     }
     wave_sync();
     stamp(7);

@@ -33,28 +33,32 @@ struct Reader {
   uint32_t end;   // bit_end - base (0 if the job starts past its buffer)
   uint32_t wpos;  // bit offset of win's MSB (multiple of 32)
   uint32_t pos;
-  uint32_t nxt;   // bits [wpos + 64, wpos + 96)
+  uint32_t nxt;   // the stored (unswapped, unmasked) word of bits [wpos + 64, wpos + 96)
   uint64_t win;   // bits [wpos, wpos + 64)
 
-  MP3G_HD_INLINE uint32_t word(uint32_t bit) const {  // bit % 32 == 0
-    if (bit >= end) return 0u;
-    const uint32_t v = __builtin_bswap32(w[bit >> 5]);
-    const uint32_t rem = end - bit;
-    return rem < 32u ? v & (~0u << (32u - rem)) : v;
+  // stored word at bit offset `bit` (a multiple of 32); nothing is loaded at
+  // or past the end
+  MP3G_HD_INLINE uint32_t load(uint32_t bit) const { return bit < end ? w[bit >> 5] : 0u; }
+  // a loaded word in bit order, zeros from the end on
+  MP3G_HD_INLINE uint32_t word(uint32_t raw, uint32_t bit) const {
+    const uint32_t v = __builtin_bswap32(raw);
+    return bit < end && end - bit < 32u ? v & (~0u << (32u - (end - bit))) : v;
   }
   MP3G_HD_INLINE void seek(uint32_t p) {
     pos = p;
     wpos = p & ~31u;
-    win = ((uint64_t)word(wpos) << 32) | word(wpos + 32);
-    nxt = word(wpos + 64);
+    win = ((uint64_t)word(load(wpos), wpos) << 32) | word(load(wpos + 32), wpos + 32);
+    nxt = load(wpos + 64);
   }
   // bits [pos, pos + 32) in the window: every read is <= 19 bits, so one step
-  // restores pos - wpos < 32
+  // restores pos - wpos < 32.  The next word is loaded a whole word ahead and
+  // only byte-swapped / masked when it is shifted in, so the load's latency
+  // overlaps ~32 bits of decoding instead of stalling right after the issue.
   MP3G_HD_INLINE void refill() {
     if (pos - wpos >= 32u) {
-      win = (win << 32) | nxt;
+      win = (win << 32) | word(nxt, wpos + 64);
       wpos += 32;
-      nxt = word(wpos + 64);
+      nxt = load(wpos + 64);
     }
   }
   MP3G_HD_INLINE uint32_t peek() const { return (uint32_t)((win << (pos - wpos)) >> 32); }
@@ -138,8 +142,12 @@ MP3G_HD_INLINE void sf_mpeg1_long(Reader& r, int slen1, int slen2, uint32_t read
 // Decodes job j (= 2 * granule + channel): scale factors and count1 into
 // gran[j / 2].ch[j % 2], the 576 lines into coef[j * 576 ..].  T / s_root /
 // s_lin: the HuffLut entries, roots and linbits (LDS on the device).
-MP3G_HD_INLINE void decode_job(const mp3g_hjob& J, uint64_t j, const uint8_t* md, mp3g_granule* gran,
+MP3G_HD_INLINE void decode_job(const mp3g_hjob& job, uint64_t j, const uint8_t* md, mp3g_granule* gran,
                                int16_t* coef, const uint32_t* T, const uint32_t* s_root, const uint32_t* s_lin) {
+  // a register copy: the coefficient / scale-factor stores below could alias
+  // the job in the compiler's eyes, which would re-load its fields from memory
+  // (with a full vmcnt wait) in every loop iteration
+  const mp3g_hjob J = job;
   int16_t* row = coef + j * MP3G_LINES;
   LineWriter out{row, 0u, 0u, 0u, 0u};
   if (J.sf_kind == MP3G_SF_NONE) {  // absent channel of a mono granule

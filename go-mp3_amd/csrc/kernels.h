@@ -38,6 +38,10 @@ hipError_t launch_granule(int variant, const ChunkDesc* d_chunks, uint32_t n_chu
                           const mp3g_state* d_state_in, mp3g_state* d_state_out, int16_t* d_pcm,
                           hipStream_t stream);
 
+// Chunks of `variant` resident per CU (one per wave for the fast kernel, one
+// per workgroup for the exact kernels), from the kernel's VGPR / LDS usage.
+int chunks_per_cu(int variant);
+
 // Main-data decode (huffman_dev.hip): one lane per (granule, channel) job.
 hipError_t launch_huffman(const mp3g_hjob* d_jobs, uint64_t n_jobs, const uint8_t* d_md, mp3g_granule* d_gran,
                           int16_t* d_coef, hipStream_t stream);

@@ -8,6 +8,8 @@
 // so all of them reach g_tab / g_fast / g_huff without relocatable device code.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "../../include/mp3g.h"
 #include "dsp_tables.h"
 #include "kernels.h"
@@ -43,6 +45,31 @@ hipError_t upload_tables(const DspTables& tables) {
   e = hipMemcpyToSymbol(HIP_SYMBOL(g_huff), lut, sizeof(HuffLut), 0, hipMemcpyHostToDevice);
   delete lut;
   return e;
+}
+
+int chunks_per_cu(int variant) {
+  hipFuncAttributes a;
+  hipError_t e;
+  int waves_per_block;
+  if (variant == kVariantFast) {
+    e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&v3::granule_fast_kernel<false>));
+    waves_per_block = v3::kWaves;
+  } else if (variant == kVariantV1) {
+    e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&v1::granule_exact_kernel));
+    waves_per_block = 4;
+  } else {
+    e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&v2::granule_fused_kernel));
+    waves_per_block = 4;
+  }
+  if (e != hipSuccess || a.numRegs <= 0) return 1;
+  // MI355X_MICROARCH.md: 512 VGPRs per lane per SIMD in granules of 8, four
+  // SIMDs and 160 KiB of LDS per CU, at most 8 waves per SIMD
+  const int vgpr = (a.numRegs + 7) / 8 * 8;
+  const int waves_per_simd = std::min(8, 512 / vgpr);
+  int blocks = waves_per_simd * 4 / waves_per_block;
+  if (a.sharedSizeBytes > 0) blocks = std::min<int>(blocks, (int)(163840 / a.sharedSizeBytes));
+  blocks = std::max(blocks, 1);
+  return variant == kVariantFast ? blocks * waves_per_block : blocks;
 }
 
 hipError_t launch_granule(int variant, const ChunkDesc* d_chunks, uint32_t n_chunks,

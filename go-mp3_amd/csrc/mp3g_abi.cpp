@@ -84,6 +84,37 @@ int ensure_device(int dev) {
   return MP3G_OK;
 }
 
+// Automatic chunk length (granules per chunk).  A chunk costs ~k + 2 (halo)
+// + 2 (prologue) granule-times, and the launch runs ~chunks / resident rounds
+// (resident = CUs x chunks per CU) plus, when it needs more than one, about
+// half a round of tail.  Minimising that picks the shortest chunks that still
+// fit one round for small batches (c2: k = 7, 10 % faster than k = 8) and
+// ~64 granules for large ones (c3: 4 % faster than k = 256; sweep measured on
+// MI355X, tools/gpu_chunks.sh).
+uint32_t auto_chunk(const mp3g_stream* streams, uint32_t n_streams, int device, uint32_t base_mode) {
+  uint64_t maxn = 0;
+  for (uint32_t s = 0; s < n_streams; s++) maxn = std::max<uint64_t>(maxn, streams[s].n_granules);
+  if (maxn == 0) return 1;
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
+  const uint64_t resident =
+      (uint64_t)cus * (uint64_t)chunks_per_cu(base_mode == MP3G_MODE_FAST ? kVariantFast : kVariantV2);
+  uint64_t best_k = 1;
+  double best = 0.0;
+  for (uint64_t k = 1; k <= maxn;) {
+    uint64_t chunks = 0;
+    for (uint32_t s = 0; s < n_streams; s++) chunks += (streams[s].n_granules + k - 1) / k;
+    const double rounds = chunks <= resident ? 1.0 : (double)chunks / (double)resident + 0.5;
+    const double cost = rounds * (double)(k + 4);
+    if (best == 0.0 || cost <= best) {
+      best = cost;
+      best_k = k;
+    }
+    k = k < 64 ? k + 1 : std::max<uint64_t>(k + 1, k * 17 / 16);
+  }
+  return (uint32_t)std::min<uint64_t>(best_k, 1u << 20);
+}
+
 }  // namespace
 
 int mp3g::abi_fail(int status, const char* what) { return fail(status, what); }
@@ -187,19 +218,12 @@ int mp3g_plan_create(int device, const mp3g_stream* streams, uint32_t n_streams,
     if (base_mode == MP3G_MODE_FAST && streams[s].first_granule + streams[s].n_granules >= (1ull << 32))
       return fail(MP3G_ERR_UNSUPPORTED, "fast mode: granule index >= 2^32");
   }
-  uint32_t k = granules_per_chunk;
-  if (k == 0) {
-    // automatic.  exact: ~2048 workgroups of 4 waves; fast: ~8192 one-wave
-    // workgroups (11 resident per CU).  Never fewer than 8 granules per chunk
-    // so the 2-granule halo stays <= 25 %.
-    const uint64_t wgs = base_mode == MP3G_MODE_FAST ? 8192 : 2048;
-    const uint64_t want = (total + wgs - 1) / wgs;
-    k = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(want, 8), 1u << 20);
-  }
   DeviceGuard guard(device);
   if (guard.err != hipSuccess) return fail(MP3G_ERR_NO_DEVICE, "hipSetDevice", guard.err);
   int st = ensure_device(device);
   if (st) return st;
+  uint32_t k = granules_per_chunk;
+  if (k == 0) k = auto_chunk(streams, n_streams, device, base_mode);
   mp3g_plan* p = new (std::nothrow) mp3g_plan;
   if (!p) return fail(MP3G_ERR_OUT_OF_MEMORY, "plan");
   p->device = device;
