@@ -246,12 +246,6 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
   const uint32_t out_first = __builtin_amdgcn_readfirstlane((uint32_t)cd.out_first);
   const uint32_t end = __builtin_amdgcn_readfirstlane((uint32_t)(cd.out_first + cd.n_out));
   const mp3g_state* sin = state_in ? state_in + cd.stream : nullptr;
-  // this chunk's descriptors as a buffer resource (SGPRs): the next granule's
-  // descriptor is prefetched through an SGPR base and 32-bit offsets, so no
-  // 64-bit pointer is kept (and spilled) in VGPRs -- a spill reload costs an
-  // s_waitcnt vmcnt(0), which would also wait for the coefficient prefetch
-  const __amdgpu_buffer_rsrc_t rs_desc = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<mp3g_granule*>(gran + w), (short)0, (int)((end - w) * sizeof(mp3g_granule)), 0x00020000);
 
   // entry state: overlap store in registers, V history as X vectors
   float st[18];
@@ -500,12 +494,25 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     const bool more = g + 1 < end;
     uint4 p0 = {0, 0, 0, 0}, p1 = p0, p2 = p0, pd = p0;
     if (more) {
-      const uint4* src = reinterpret_cast<const uint4*>(coef + (size_t)(g + 1) * MP3G_COEF_PER_GRANULE);
-      p0 = src[lane];
-      p1 = src[lane + 64];
-      if (lane < 16) p2 = src[lane + 128];
+      // the next granule through per-granule buffer resources (SGPR bases,
+      // 32-bit lane offsets): no 64-bit pointer is kept (and spilled) in VGPRs
+      // -- a spill reload costs an s_waitcnt vmcnt(0), which would also wait
+      // for this prefetch
+      const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<int16_t*>(coef + (size_t)(g + 1) * MP3G_COEF_PER_GRANULE), (short)0,
+          (int)(MP3G_COEF_PER_GRANULE * sizeof(int16_t)), 0x00020000);
+      const auto q0 = __builtin_amdgcn_raw_buffer_load_b128(rc, lane * 16, 0, 0);
+      const auto q1 = __builtin_amdgcn_raw_buffer_load_b128(rc, lane * 16 + 1024, 0, 0);
+      p0 = make_uint4(q0[0], q0[1], q0[2], q0[3]);
+      p1 = make_uint4(q1[0], q1[1], q1[2], q1[3]);
+      if (lane < 16) {
+        const auto q2 = __builtin_amdgcn_raw_buffer_load_b128(rc, lane * 16 + 2048, 0, 0);
+        p2 = make_uint4(q2[0], q2[1], q2[2], q2[3]);
+      }
       if (lane < 10) {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs_desc, lane * 16, (int)((g + 1 - w) * sizeof(mp3g_granule)), 0);
+        const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<mp3g_granule*>(gran + g + 1), (short)0, (int)sizeof(mp3g_granule), 0x00020000);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rd, lane * 16, 0, 0);
         pd = make_uint4(v[0], v[1], v[2], v[3]);
       }
     }

@@ -86,11 +86,11 @@ int ensure_device(int dev) {
 
 // Automatic chunk length (granules per chunk).  A chunk costs ~k + 2 (halo)
 // + 2 (prologue) granule-times, and the launch runs ~chunks / resident rounds
-// (resident = CUs x chunks per CU) plus, when it needs more than one, about
-// half a round of tail.  Minimising that picks the shortest chunks that still
-// fit one round for small batches (c2: k = 7, 10 % faster than k = 8) and
-// ~64 granules for large ones (c3: 4 % faster than k = 256; sweep measured on
-// MI355X, tools/gpu_chunks.sh).
+// (resident = CUs x chunks per CU) plus about half a round of tail (chunks
+// finish at different times).  Minimising that picks k = 7 for c2 (10 %
+// faster than k = 8) and ~64 granules for c3 (4 % faster than k = 256, 20 %
+// faster than one round of 683-granule chunks; sweeps measured on MI355X,
+// tools/gpu_chunks.sh).
 uint32_t auto_chunk(const mp3g_stream* streams, uint32_t n_streams, int device, uint32_t base_mode) {
   uint64_t maxn = 0;
   for (uint32_t s = 0; s < n_streams; s++) maxn = std::max<uint64_t>(maxn, streams[s].n_granules);
@@ -104,7 +104,7 @@ uint32_t auto_chunk(const mp3g_stream* streams, uint32_t n_streams, int device, 
   for (uint64_t k = 1; k <= maxn;) {
     uint64_t chunks = 0;
     for (uint32_t s = 0; s < n_streams; s++) chunks += (streams[s].n_granules + k - 1) / k;
-    const double rounds = chunks <= resident ? 1.0 : (double)chunks / (double)resident + 0.5;
+    const double rounds = (double)chunks / (double)resident + 0.5;
     const double cost = rounds * (double)(k + 4);
     if (best == 0.0 || cost <= best) {
       best = cost;
