@@ -16,23 +16,25 @@ import sys
 KERNEL = "granule"
 
 
-def counters(d):
+def counters(d, kernel=None):
+    kernel = kernel or KERNEL
     f = glob.glob(os.path.join(d, "*counter_collection.csv"))
     agg = collections.defaultdict(list)
     if f:
         for r in csv.DictReader(open(f[0])):
-            if KERNEL in r["Kernel_Name"]:
+            if kernel in r["Kernel_Name"]:
                 agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
 
-def main(src, tag, cfg, dst="profiles", bytes_per_launch=None):
+def main(src, tag, cfg, dst="profiles", bytes_per_launch=None, kernel=None, suffix=""):
+    kernel = kernel or KERNEL
     base = os.path.join(src, f"prof_{tag}_{cfg}")
     stats = list(csv.DictReader(open(glob.glob(base + "_trace/*kernel_stats.csv")[0])))
-    k = [r for r in stats if KERNEL in r["Name"]][0]
-    fetch = counters(base + "_fetch").get("FETCH_SIZE")
-    write = counters(base + "_write").get("WRITE_SIZE")
-    sq = counters(base + "_sq")
+    k = [r for r in stats if kernel in r["Name"]][0]
+    fetch = counters(base + "_fetch", kernel).get("FETCH_SIZE")
+    write = counters(base + "_write", kernel).get("WRITE_SIZE")
+    sq = counters(base + "_sq", kernel)
     avg_ns = float(k["AverageNs"])
     out = {"tag": tag, "config": cfg, "kernel": k["Name"].split("(")[0], "calls": int(k["Calls"]),
            "avg_ns": avg_ns, "min_ns": float(k["MinNs"]), "max_ns": float(k["MaxNs"])}
@@ -52,7 +54,7 @@ def main(src, tag, cfg, dst="profiles", bytes_per_launch=None):
         out["algorithmic_bytes_per_launch"] = bytes_per_launch
         out["algorithmic_gbps"] = bytes_per_launch / avg_ns
     os.makedirs(dst, exist_ok=True)
-    json.dump(out, open(os.path.join(dst, f"{tag}_{cfg}.json"), "w"), indent=1)
+    json.dump(out, open(os.path.join(dst, f"{tag}_{cfg}{suffix}.json"), "w"), indent=1)
     for kind in ("trace",):
         for f in glob.glob(base + f"_{kind}/*kernel_stats.csv"):
             shutil.copyfile(f, os.path.join(dst, f"{tag}_{cfg}_kernel_stats.csv"))
@@ -61,5 +63,6 @@ def main(src, tag, cfg, dst="profiles", bytes_per_launch=None):
 
 if __name__ == "__main__":
     src, tag, cfg = sys.argv[1:4]
-    bpl = int(sys.argv[4]) if len(sys.argv) > 4 else None
-    main(src, tag, cfg, bytes_per_launch=bpl)
+    bpl = int(sys.argv[4]) if len(sys.argv) > 4 and sys.argv[4] != "-" else None
+    kern = sys.argv[5] if len(sys.argv) > 5 else None
+    main(src, tag, cfg, bytes_per_launch=bpl, kernel=kern, suffix=("_" + kern) if kern else "")
