@@ -152,6 +152,7 @@ def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle):
            # 2 x 1152 B coefficients + 2 x 63 B scale factors / count1 out per granule
            "huffman_algorithmic_bytes_per_launch": md + n * (96 + 2304 + 126),
            "huffman_algorithmic_gbps": round((md + n * (96 + 2304 + 126)) / (huff_ms * 1e-3) / 1e9, 2),
+           "huffman_traffic_bytes_per_launch": profiled_traffic(cfg, "mp3g::huff::huffman_kernel")[0],
            "main_data_bytes": md, "bitstream_bytes": int(sum(len(d) for d in datas)),
            "host_scan_s": round(scan_s, 4), "host_scan_frames_per_s": round(frames / scan_s, 1),
            "host_scan_threads": 16, "writer_s": round(writer_s, 2)}
@@ -166,12 +167,18 @@ def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle):
     return out
 
 
+PROFILE_TAG = "r01h"  # profiles/<tag>_<cfg>_<kernel>.json of the current kernels
+
+
 def profiled_traffic(cfg, kernel):
     """HBM bytes per launch from the newest rocprofv3 PMC summary in profiles/
     for this config and kernel (FETCH_SIZE x2 + WRITE_SIZE, KiB -> B;
     tools/summarize_profile.py), or None."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_{cfg}.json")))
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_{cfg}*.json")))
+    # the current profile set first, then older ones (newest name last)
+    files = [f for f in files if not os.path.basename(f).startswith(PROFILE_TAG + "_")] + \
+        [f for f in files if os.path.basename(f).startswith(PROFILE_TAG + "_")]
     for f in reversed(files):
         d = json.load(open(f))
         if kernel in d.get("kernel", "") and d.get("hbm_bytes_per_launch_corrected"):

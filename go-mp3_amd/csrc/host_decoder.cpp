@@ -65,7 +65,9 @@ St parse_all(const uint8_t* data, size_t len, std::vector<mp3g_granule>* g, std:
 struct mp3g_decoder {
   std::vector<uint8_t> data;  // own copy: no caller pointer is retained
   host::Source src;
-  host::FrameParser parser;
+  host::FrameParser parser;    // MP3G_FLAG_HOST_HUFFMAN: full host parse
+  host::FrameScanner scanner;  // default: host scan + GPU main-data kernel
+  std::vector<uint8_t> md;     // main-data concatenation the scanner's jobs address
   int device = 0;
   uint32_t mode = 0;
   int sample_rate = 0;
@@ -85,10 +87,13 @@ struct mp3g_decoder {
   int16_t* d_coef = nullptr;
   int16_t* d_pcm = nullptr;
   mp3g_state* d_state = nullptr;  // [0] = carried in, [1] = out
-  size_t cap_granules = 0;
+  mp3g_hjob* d_jobs = nullptr;
+  uint8_t* d_md = nullptr;
+  size_t cap_granules = 0, cap_md = 0;
   // host staging
   std::vector<mp3g_granule> h_gran;
   std::vector<int16_t> h_coef;
+  std::vector<mp3g_hjob> h_jobs;
   std::vector<int16_t> h_pcm;
   std::vector<uint32_t> frame_pcm_bytes;  // PCM bytes of each frame of the last batch
   std::vector<size_t> frame_ends;         // end offset in buf of each buffered frame
@@ -98,7 +103,7 @@ struct mp3g_decoder {
     int prev = -1;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(device);
-    for (void* p : {(void*)d_gran, (void*)d_coef, (void*)d_pcm, (void*)d_state})
+    for (void* p : {(void*)d_gran, (void*)d_coef, (void*)d_pcm, (void*)d_state, (void*)d_jobs, (void*)d_md})
       if (p) (void)hipFree(p);
     if (stream) (void)hipStreamDestroy(stream);
     if (prev >= 0) (void)hipSetDevice(prev);
@@ -107,11 +112,12 @@ struct mp3g_decoder {
   int ensure_capacity(size_t n) {
     if (n <= cap_granules) return MP3G_OK;
     size_t cap = std::max<size_t>(n, cap_granules * 2);
-    for (void** p : {(void**)&d_gran, (void**)&d_coef, (void**)&d_pcm})
+    for (void** p : {(void**)&d_gran, (void**)&d_coef, (void**)&d_pcm, (void**)&d_jobs})
       if (*p) { (void)hipFree(*p); *p = nullptr; }
     if (hipMalloc(&d_gran, cap * sizeof(mp3g_granule)) != hipSuccess ||
         hipMalloc(&d_coef, cap * MP3G_COEF_PER_GRANULE * sizeof(int16_t)) != hipSuccess ||
-        hipMalloc(&d_pcm, cap * MP3G_PCM_BYTES_PER_GRANULE) != hipSuccess) {
+        hipMalloc(&d_pcm, cap * MP3G_PCM_BYTES_PER_GRANULE) != hipSuccess ||
+        hipMalloc(&d_jobs, 2 * cap * sizeof(mp3g_hjob)) != hipSuccess) {
       cap_granules = 0;
       return abi_fail(MP3G_ERR_OUT_OF_MEMORY, "decoder device buffers");
     }
@@ -122,23 +128,46 @@ struct mp3g_decoder {
   // Parses up to `max_frames` frames and decodes them on the device,
   // appending their PCM to buf.  Returns MP3G_OK if at least one frame was
   // decoded (a later parse error is kept in `pending`), else the error.
+  bool gpu_huffman() const { return (mode & MP3G_FLAG_HOST_HUFFMAN) == 0; }
+
   int decode_batch(size_t max_frames) {
     h_gran.clear();
     h_coef.clear();
+    h_jobs.clear();
     frame_pcm_bytes.clear();
-    host::ParsedFrame f;
     St st = St::kOk;
-    for (size_t i = 0; i < max_frames; i++) {
-      st = parser.next(src, &f);
-      if (st != St::kOk) break;
-      for (int gr = 0; gr < f.n_granules; gr++) {
-        h_gran.push_back(f.gran[gr]);
-        h_coef.insert(h_coef.end(), f.coef[gr], f.coef[gr] + MP3G_COEF_PER_GRANULE);
+    if (gpu_huffman()) {
+      // drop main data no later frame can reach (the reservoir is < 2 KB)
+      const int64_t dead = scanner.live_start(md);
+      if (dead > 0) {
+        md.erase(md.begin(), md.begin() + dead);
+        scanner.drop(dead);
       }
-      frame_pcm_bytes.push_back((uint32_t)(f.n_granules * MP3G_PCM_BYTES_PER_GRANULE));
+      host::ScannedFrame f;
+      for (size_t i = 0; i < max_frames; i++) {
+        st = scanner.next(src, &f, &md);
+        if (st != St::kOk) break;
+        for (int gr = 0; gr < f.n_granules; gr++) {
+          h_gran.push_back(f.gran[gr]);
+          h_jobs.push_back(f.job[gr][0]);
+          h_jobs.push_back(f.job[gr][1]);
+        }
+        frame_pcm_bytes.push_back((uint32_t)(f.n_granules * MP3G_PCM_BYTES_PER_GRANULE));
+      }
+    } else {
+      host::ParsedFrame f;
+      for (size_t i = 0; i < max_frames; i++) {
+        st = parser.next(src, &f);
+        if (st != St::kOk) break;
+        for (int gr = 0; gr < f.n_granules; gr++) {
+          h_gran.push_back(f.gran[gr]);
+          h_coef.insert(h_coef.end(), f.coef[gr], f.coef[gr] + MP3G_COEF_PER_GRANULE);
+        }
+        frame_pcm_bytes.push_back((uint32_t)(f.n_granules * MP3G_PCM_BYTES_PER_GRANULE));
+      }
     }
     const int err = st == St::kOk ? MP3G_OK : to_status(st);
-    if (err != MP3G_OK) parser.reset();  // d.frame = nil after a failed frame.Read
+    if (err != MP3G_OK) reset_reservoir();  // d.frame = nil after a failed frame.Read
     if (h_gran.empty()) {
       fresh = true;
       return err;
@@ -150,6 +179,11 @@ struct mp3g_decoder {
       fresh = true;  // the frame after a failed one starts from zero state
     }
     return MP3G_OK;
+  }
+
+  void reset_reservoir() {
+    parser.reset();
+    scanner.reset();
   }
 
   int run_device() {
@@ -169,11 +203,32 @@ struct mp3g_decoder {
     if (rc) return rc;
     mp3g_stream s{0, (uint32_t)n, (fresh ? 0u : (uint32_t)MP3G_STREAM_STATE_IN) | MP3G_STREAM_STATE_OUT};
     mp3g_plan* plan = nullptr;
-    rc = mp3g_plan_create(device, &s, 1, 0, mode, &plan);
+    rc = mp3g_plan_create(device, &s, 1, 0, mode & ~(uint32_t)MP3G_FLAG_HOST_HUFFMAN, &plan);
     if (rc) return rc;
     hipError_t e = hipMemcpyAsync(d_gran, h_gran.data(), n * sizeof(mp3g_granule), hipMemcpyHostToDevice, stream);
-    if (e == hipSuccess)
+    if (gpu_huffman()) {
+      // main data + jobs up, then scale factors / Huffman codes on the device
+      const size_t mdb = md.size() + 16;  // + padding for the 32-bit window loads
+      if (e == hipSuccess && mdb > cap_md) {
+        if (d_md) (void)hipFree(d_md);
+        d_md = nullptr;
+        cap_md = std::max(mdb, 2 * cap_md);
+        e = hipMalloc(&d_md, cap_md);
+        if (e != hipSuccess) cap_md = 0;
+      }
+      if (e == hipSuccess && !md.empty()) e = hipMemcpyAsync(d_md, md.data(), md.size(), hipMemcpyHostToDevice, stream);
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(d_jobs, h_jobs.data(), h_jobs.size() * sizeof(mp3g_hjob), hipMemcpyHostToDevice, stream);
+      if (e == hipSuccess) {
+        rc = mp3g_huffman_execute(device, d_jobs, n, d_md, d_gran, d_coef, stream);
+        if (rc) {
+          mp3g_plan_destroy(plan);
+          return rc;
+        }
+      }
+    } else if (e == hipSuccess) {
       e = hipMemcpyAsync(d_coef, h_coef.data(), h_coef.size() * sizeof(int16_t), hipMemcpyHostToDevice, stream);
+    }
     if (e != hipSuccess) {
       mp3g_plan_destroy(plan);
       return abi_fail(MP3G_ERR_DEVICE, "decoder H2D copy");
@@ -384,7 +439,8 @@ int mp3g_decoder_seek(mp3g_decoder* d, int64_t offset, int whence, int64_t* newp
   }
   d->pos = npos;
   d->buf_reset();
-  d->parser.reset();  // d.frame = nil
+  d->reset_reservoir();  // d.frame = nil
+  d->md.clear();
   d->fresh = true;
   d->pending = MP3G_OK;
   d->batch_frames = 16;

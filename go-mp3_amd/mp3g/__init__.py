@@ -13,7 +13,7 @@ import os
 import numpy as np
 
 __all__ = ["CHANNEL_DTYPE", "GRANULE_DTYPE", "STREAM_DTYPE", "STATE_DTYPE", "MODE_EXACT",
-           "MODE_FAST", "FLAG_CHECKED", "FLAG_KERNEL_V1", "STATE_IN", "STATE_OUT", "Mp3gError", "lib", "lib_path",
+           "MODE_FAST", "FLAG_CHECKED", "FLAG_KERNEL_V1", "FLAG_HOST_HUFFMAN", "STATE_IN", "STATE_OUT", "Mp3gError", "lib", "lib_path",
            "decode_host", "validate", "Plan", "device_count", "streams_for", "parse_stream",
            "parse_streams", "Decoder", "HJOB_DTYPE", "scan_streams", "huffman_execute", "decode_streams"]
 
@@ -37,7 +37,7 @@ HJOB_DTYPE = np.dtype([("part2_start", "<u8"), ("bit_end", "<u8"), ("scf0_delta"
 assert CHANNEL_DTYPE.itemsize == 72 and GRANULE_DTYPE.itemsize == 160 and HJOB_DTYPE.itemsize == 48
 assert STREAM_DTYPE.itemsize == 16 and STATE_DTYPE.itemsize == 12800
 
-MODE_EXACT, MODE_FAST, FLAG_CHECKED, FLAG_KERNEL_V1 = 0, 1, 0x100, 0x200
+MODE_EXACT, MODE_FAST, FLAG_CHECKED, FLAG_KERNEL_V1, FLAG_HOST_HUFFMAN = 0, 1, 0x100, 0x200, 0x400
 STATE_IN, STATE_OUT = 1, 2
 STATUS = {0: "ok", 1: "invalid argument", 2: "invalid granule", 3: "no device", 4: "device error",
           5: "out of memory", 6: "parse error", 7: "eof", 8: "unsupported"}

@@ -120,6 +120,8 @@ typedef struct mp3g_stream {
 #define MP3G_MODE_FAST  1u   /* MFMA/fast-transform polyphase; |dPCM| <= 1 LSB          */
 #define MP3G_FLAG_CHECKED 0x100u /* validate descriptor ranges on the host first      */
 #define MP3G_FLAG_KERNEL_V1 0x200u /* exact mode via the per-phase v1 kernel (cross-check) */
+#define MP3G_FLAG_HOST_HUFFMAN 0x400u /* decoder: scale factors + Huffman on the host (mp3g_parse_*)
+                                         instead of the GPU main-data kernel (cross-check) */
 
 /* ---- library / device ---------------------------------------------------- */
 int mp3g_abi_version(void);
@@ -260,8 +262,10 @@ int mp3g_decode_streams(int device, uint32_t n_streams, const uint8_t* const* da
                         mp3g_stream* streams, int* end_status);
 
 /* ---- decoder: mp3.NewDecoder / io.Reader / io.Seeker (decode.go:27-388) ----
- * Parses on the host with read-ahead and decodes batches of frames on
- * `device` (mode = MP3G_MODE_EXACT | MP3G_MODE_FAST).  `data` is copied.
+ * Scans on the host with read-ahead (headers, side info, reservoir) and
+ * decodes batches of frames on `device`: scale factors + Huffman codes with
+ * the main-data kernel, then the DSP (mode = MP3G_MODE_EXACT | MP3G_MODE_FAST,
+ * | MP3G_FLAG_HOST_HUFFMAN for the host parse instead of the Huffman kernel).  `data` is copied.
  * seekable = 0 models a reader that is not an io.Seeker (Length = -1).
  * Read returns MP3G_OK with *n >= 1, MP3G_EOF, or the error of the frame
  * that failed (after all PCM before it was delivered) -- like Decoder.Read. */

@@ -1,6 +1,8 @@
 """The decoder API of the product (mp3g_decoder_*: mp3.NewDecoder / Read /
 Seek / time API, reference decode.go:27-388) on the GPU vs the oracle's
-Decoder, operation by operation.
+Decoder, operation by operation.  By default the decoder runs the host scan
++ GPU main-data kernel + GPU DSP; the host-parse
+variant (MP3G_FLAG_HOST_HUFFMAN) is cross-checked too.
 
 Exact mode: every Read returns the same status and the same bytes as the
 oracle, every Seek the same status and position (bit-exact PCM across the
@@ -32,9 +34,10 @@ def read_all_both(d, o):
 
 
 @pytest.mark.parametrize("name", ["classic_lame.mp3", "mpeg2.mp3"])
-def test_read_all_exact(gpu, sample_files, golden, name):
+@pytest.mark.parametrize("host_huffman", [False, True])
+def test_read_all_exact(gpu, sample_files, golden, name, host_huffman):
     import hashlib
-    d, o = both(gpu, sample_files[name])
+    d, o = both(gpu, sample_files[name], mode=gpu.FLAG_HOST_HUFFMAN if host_huffman else 0)
     assert (d.sample_rate, d.length, d.bytes_per_frame) == (o.sample_rate, o.length, o.bytes_per_frame)
     assert d.duration_ns == o.duration_ns
     b, b2 = read_all_both(d, o)
@@ -51,9 +54,9 @@ def test_read_all_fast(gpu, sample_files, name):
     assert diff.max() <= 1 and (diff > 0).mean() < 0.01
 
 
-@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("mode", [0, 1, 0x400])
 def test_random_seek_read_sequence(gpu, sample_files, mode):
-    rng = np.random.default_rng(7 + mode)
+    rng = np.random.default_rng(7 + mode % 2)
     for name in ("classic_lame.mp3", "mpeg2.mp3"):
         d, o = both(gpu, sample_files[name], mode=mode)
         L = o.length
@@ -64,7 +67,7 @@ def test_random_seek_read_sequence(gpu, sample_files, mode):
                 st, b = d.read(n)
                 st2, b2 = o.read(n)
                 assert st == ST[st2] and len(b) == len(b2), (name, step, st, st2)
-                if mode == 0:
+                if mode != 1:
                     assert b == b2, (name, step)
                 elif b:
                     diff = np.abs(np.frombuffer(b[:len(b) // 2 * 2], np.int16).astype(np.int32)
