@@ -6,8 +6,12 @@
 // + count1 into the granule descriptor (whose side-info fields the scan
 // filled) and the channel's 576 int16 coefficients (huffman_job.h).
 // Decoding inside a channel is bit-serial; the parallelism is across jobs
-// (two per granule, 64 per wave; neighbouring lanes read neighbouring
-// main-data bytes).  The Huffman tables (huff_lut.h, 18 KB) live in LDS.
+// (two per granule, 64 per wave).  A wave's 64 consecutive jobs read one
+// contiguous span of the main data: the wave stages it in LDS with coalesced
+// 8-byte loads (byte-swapped once), so the bit-serial loop never waits on
+// global memory (on gfx9 a load's vmcnt wait would also wait for the
+// coefficient stores issued before it).  The Huffman tables (huff_lut.h,
+// 18 KB) live in LDS too.
 // (compiled as part of kernels.hip)
 #include "huffman_job.h"
 
@@ -15,22 +19,64 @@ namespace mp3g {
 namespace huff {
 
 constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / 64;
+// Main data staged per wave: 64 consecutive jobs (16 MPEG-1 stereo frames)
+// span ~6.1 KB at 128 kbps.  7.5 KB per wave keeps the block at 48 KB of
+// LDS (3 blocks = 12 waves per CU); a wave whose span does not fit reads
+// straight from global memory.
+constexpr int kStageWords = 960;
+
+__device__ __forceinline__ uint64_t wave_min(uint64_t v) {
+  for (int o = 32; o; o >>= 1) {
+    const uint64_t u = __shfl_xor(v, o, 64);
+    v = u < v ? u : v;
+  }
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_max(uint64_t v) {
+  for (int o = 32; o; o >>= 1) {
+    const uint64_t u = __shfl_xor(v, o, 64);
+    v = u > v ? u : v;
+  }
+  return v;
+}
 
 __global__ void __launch_bounds__(kThreads)
 huffman_kernel(const mp3g_hjob* __restrict__ jobs, uint64_t n_jobs, const uint8_t* __restrict__ md,
                mp3g_granule* __restrict__ gran, int16_t* __restrict__ coef) {
   __shared__ uint32_t T[kHuffMaxEntries];
   __shared__ uint32_t s_root[34], s_lin[34];
+  __shared__ uint64_t stage[kWaves][kStageWords];
   const uint32_t n_e = g_huff.n_entries;
   for (uint32_t i = threadIdx.x; i < n_e; i += kThreads) T[i] = g_huff.e[i];
   if (threadIdx.x < 34) {
     s_root[threadIdx.x] = g_huff.root[threadIdx.x];
     s_lin[threadIdx.x] = g_huff.linbits[threadIdx.x];
   }
-  __syncthreads();
   const uint64_t j = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (j >= n_jobs) return;
-  decode_job(jobs[j], j, md, gran, coef, T, s_root, s_lin);
+  const bool valid = j < n_jobs;
+  mp3g_hjob J{};
+  if (valid) J = jobs[j];
+  // the wave's main-data span [lo, hi) in bits, lo 64-bit aligned
+  const bool reads = valid && J.sf_kind != MP3G_SF_NONE;
+  const uint64_t base = job_base(J);
+  const uint64_t lo = wave_min(reads ? base : ~0ull);
+  const uint64_t hi = wave_max(reads ? J.bit_end : 0ull);
+  const uint64_t nwords = hi > lo && lo != ~0ull ? ((hi - lo + 63) >> 6) : 0ull;
+  const bool staged = nwords <= (uint64_t)kStageWords;  // wave-uniform
+  const int wv = threadIdx.x >> 6;
+  if (staged) {
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(md + (lo >> 3));
+    for (uint32_t k = threadIdx.x & 63; k < (uint32_t)nwords; k += 64) stage[wv][k] = bswap64(src[k]);
+  }
+  __syncthreads();
+  if (!valid) return;
+  if (staged) {
+    const uint32_t off = reads ? (uint32_t)((base - lo) >> 6) : 0u;
+    decode_job<false>(J, j, &stage[wv][off], (uint32_t)nwords - off, gran, coef, T, s_root, s_lin);
+  } else {
+    decode_job_direct(J, j, md, gran, coef, T, s_root, s_lin);
+  }
 }
 
 }  // namespace huff

@@ -25,48 +25,62 @@
 namespace mp3g {
 namespace huff {
 
-// Big-endian reader over the main-data buffer.  Positions are 32-bit offsets
-// from `w`, a 32-bit-aligned bit position at or before every bit the job
-// reads (a frame's bit buffer spans at most a few KiB: host_parse.cpp).
-struct Reader {
-  const uint32_t* w;
-  uint32_t end;   // bit_end - base (0 if the job starts past its buffer)
-  uint32_t wpos;  // bit offset of win's MSB (multiple of 32)
-  uint32_t pos;
-  uint32_t nxt;   // the stored (unswapped, unmasked) word of bits [wpos + 64, wpos + 96)
-  uint64_t win;   // bits [wpos, wpos + 64)
+MP3G_HD_INLINE uint64_t bswap64(uint64_t v) { return __builtin_bswap64(v); }
 
-  // stored word at bit offset `bit` (a multiple of 32); nothing is loaded at
-  // or past the end
-  MP3G_HD_INLINE uint32_t load(uint32_t bit) const { return bit < end ? w[bit >> 5] : 0u; }
-  // a loaded word in bit order, zeros from the end on
-  MP3G_HD_INLINE uint32_t word(uint32_t raw, uint32_t bit) const {
-    const uint32_t v = __builtin_bswap32(raw);
-    return bit < end && end - bit < 32u ? v & (~0u << (32u - (end - bit))) : v;
-  }
+// Big-endian reader over the main-data buffer, 64 bits at a time.  `w` is
+// the job's word 0 (bit `base` of the concatenated main data, a multiple of
+// 64); only words [0, nw) are loaded, others read as 0.  kSwap: the words
+// are stored in stream byte order (global memory) and swapped on load; the
+// LDS staging copy (huffman_dev.hip) is swapped once when it is filled.
+// Bits past `end` are only masked where a read could reach them (the slow
+// paths); the fast paths first check that they stay below `end`.
+template <bool kSwap>
+struct Reader {
+  const uint64_t* w;
+  uint32_t nw;
+  uint32_t end;   // bit_end - base (0 if the job starts past its buffer)
+  uint32_t wpos;  // bit offset of win's MSB (multiple of 64)
+  uint32_t pos;
+  uint64_t win;   // bits [wpos, wpos + 64)
+  uint64_t nxt;   // bits [wpos + 64, wpos + 128)
+  uint64_t nn;    // the stored word of bits [wpos + 128, wpos + 192), in flight
+
+  MP3G_HD_INLINE uint64_t load(uint32_t k) const { return k < nw ? w[k] : 0ull; }
+  MP3G_HD_INLINE static uint64_t order(uint64_t raw) { return kSwap ? bswap64(raw) : raw; }
   MP3G_HD_INLINE void seek(uint32_t p) {
     pos = p;
-    wpos = p & ~31u;
-    win = ((uint64_t)word(load(wpos), wpos) << 32) | word(load(wpos + 32), wpos + 32);
-    nxt = load(wpos + 64);
+    wpos = p & ~63u;
+    win = order(load(wpos >> 6));
+    nxt = order(load((wpos >> 6) + 1));
+    nn = load((wpos >> 6) + 2);
   }
-  // bits [pos, pos + 32) in the window: every read is <= 19 bits, so one step
-  // restores pos - wpos < 32.  The next word is loaded a whole word ahead and
-  // only byte-swapped / masked when it is shifted in, so the load's latency
-  // overlaps ~32 bits of decoding instead of stalling right after the issue.
+  // restores pos - wpos < 64 after at most 64 bits were consumed since the
+  // last call.  The next word is loaded two words ahead, so its latency
+  // overlaps ~64 bits of decoding.
   MP3G_HD_INLINE void refill() {
-    if (pos - wpos >= 32u) {
-      win = (win << 32) | word(nxt, wpos + 64);
-      wpos += 32;
-      nxt = load(wpos + 64);
+    if (pos - wpos >= 64u) {
+      win = nxt;
+      nxt = order(nn);
+      wpos += 64;
+      nn = load((wpos >> 6) + 2);
     }
   }
-  MP3G_HD_INLINE uint32_t peek() const { return (uint32_t)((win << (pos - wpos)) >> 32); }
+  // the 64 stream bits from pos (not masked at the end)
+  MP3G_HD_INLINE uint64_t peek64() const {
+    const uint32_t sh = pos - wpos;
+    return (win << sh) | ((nxt >> 1) >> (63u - sh));
+  }
+  // the same with zeros from `end` on (bits.Bit past the end, bits.go:45-56)
+  MP3G_HD_INLINE uint64_t peek64m() const {
+    const uint32_t left = end > pos ? end - pos : 0u;
+    const uint64_t v = peek64();
+    return left >= 64u ? v : v & ~(~0ull >> left);
+  }
   // bits.Bits(n), 1 <= n <= 13: 0 and no advance if it would pass the end
   MP3G_HD_INLINE uint32_t bits(int n) {
     refill();
     if (pos + (uint32_t)n > end) return 0u;
-    const uint32_t v = peek() >> (32 - n);
+    const uint32_t v = (uint32_t)(peek64() >> (64 - n));
     pos += (uint32_t)n;
     return v;
   }
@@ -74,17 +88,15 @@ struct Reader {
   MP3G_HD_INLINE uint32_t bit() {
     refill();
     if (pos >= end) return 0u;
-    const uint32_t v = peek() >> 31;
+    const uint32_t v = (uint32_t)(peek64() >> 63);
     pos++;
     return v;
   }
 };
 
-// huffman.Decode's tree walk: the leaf the next bits reach (zeros past the
-// end) and the advance of its Bit() calls, min(len, end - pos).
-MP3G_HD_INLINE uint32_t decode_xy(Reader& r, const uint32_t* T, uint32_t root) {
-  r.refill();
-  const uint32_t p = r.peek();
+// The leaf the 32 stream bits `p` reach in the table at `root`; *len = its
+// codeword length.
+MP3G_HD_INLINE uint32_t lut_leaf(const uint32_t* T, uint32_t root, uint32_t p, uint32_t* len) {
   int used = (int)(root >> 24);
   uint32_t e = T[(root & 0xffffffu) + (p >> (32 - used))];
   while (e & 0x80000000u) {
@@ -92,9 +104,96 @@ MP3G_HD_INLINE uint32_t decode_xy(Reader& r, const uint32_t* T, uint32_t root) {
     e = T[(e & 0xffffffu) + ((p << used) >> (32 - wd))];
     used += wd;
   }
-  const uint32_t len = (e >> 8) & 31u;
-  if (r.pos < r.end) r.pos = r.pos + len < r.end ? r.pos + len : r.end;
+  *len = (e >> 8) & 31u;
   return e & 255u;
+}
+
+// huffman.Decode's tree walk near the end of the buffer: the leaf the next
+// bits reach (zeros past the end) and the advance of its Bit() calls,
+// min(len, end - pos).
+template <bool kSwap>
+MP3G_HD_INLINE uint32_t decode_xy(Reader<kSwap>& r, const uint32_t* T, uint32_t root) {
+  r.refill();
+  uint32_t len;
+  const uint32_t xy = lut_leaf(T, root, (uint32_t)(r.peek64m() >> 32), &len);
+  if (r.pos < r.end) r.pos = r.pos + len < r.end ? r.pos + len : r.end;
+  return xy;
+}
+
+// One big-values pair (maindata/huffman.go:66-104): codeword, x linbits,
+// x sign, y linbits, y sign.  Far from the end (<= 19 + 2 * 14 = 47 bits to
+// go) every field comes out of one 64-bit peek; otherwise each read follows
+// the reference's clamping.
+template <bool kSwap>
+MP3G_HD_INLINE void decode_pair(Reader<kSwap>& r, const uint32_t* T, uint32_t root, int lb, int& xo, int& yo) {
+  r.refill();
+  int x, y;
+  if (r.pos + 47u <= r.end) {
+    const uint64_t p64 = r.peek64();
+    uint32_t len;
+    const uint32_t xy = lut_leaf(T, root, (uint32_t)(p64 >> 32), &len);
+    x = (int)(xy >> 4);
+    y = (int)(xy & 15u);
+    const uint32_t q = (uint32_t)((p64 << len) >> 32);  // the <= 28 bits after the codeword
+    const int lbs = lb ? lb : 1;
+    uint32_t o = 0;
+    if (lb && x == 15) {
+      x += (int)(q >> (32 - lbs));
+      o = (uint32_t)lb;
+    }
+    if (x) {
+      x = ((q << o) >> 31) ? -x : x;
+      o++;
+    }
+    if (lb && y == 15) {
+      y += (int)((q << o) >> (32 - lbs));
+      o += (uint32_t)lb;
+    }
+    if (y) {
+      y = ((q << o) >> 31) ? -y : y;
+      o++;
+    }
+    r.pos += len + o;
+  } else {
+    const uint32_t xy = decode_xy(r, T, root);
+    x = (int)(xy >> 4);
+    y = (int)(xy & 15u);
+    if (lb && x == 15) x += (int)r.bits(lb);
+    if (x && r.bit()) x = -x;
+    if (lb && y == 15) y += (int)r.bits(lb);
+    if (y && r.bit()) y = -y;
+  }
+  xo = x;
+  yo = y;
+}
+
+// One count1 quad (maindata/huffman.go:106-131): codeword <= 6 bits + 4 signs.
+template <bool kSwap>
+MP3G_HD_INLINE uint32_t decode_quad(Reader<kSwap>& r, const uint32_t* T, uint32_t root, int& v, int& w, int& x,
+                                    int& y) {
+  r.refill();
+  uint32_t q;
+  if (r.pos + 10u <= r.end) {
+    const uint64_t p64 = r.peek64();
+    uint32_t len;
+    q = lut_leaf(T, root, (uint32_t)(p64 >> 32), &len) & 15u;
+    const uint32_t s = (uint32_t)((p64 << len) >> 32);
+    v = (int)((q >> 3) & 1u), w = (int)((q >> 2) & 1u), x = (int)((q >> 1) & 1u), y = (int)(q & 1u);
+    uint32_t o = 0;
+    if (v) v = ((s << o++) >> 31) ? -1 : 1;
+    if (w) w = ((s << o++) >> 31) ? -1 : 1;
+    if (x) x = ((s << o++) >> 31) ? -1 : 1;
+    if (y) y = ((s << o++) >> 31) ? -1 : 1;
+    r.pos += len + o;
+  } else {
+    q = decode_xy(r, T, root) & 15u;
+    v = (int)((q >> 3) & 1u), w = (int)((q >> 2) & 1u), x = (int)((q >> 1) & 1u), y = (int)(q & 1u);
+    if (v && r.bit()) v = -v;
+    if (w && r.bit()) w = -w;
+    if (x && r.bit()) x = -x;
+    if (y && r.bit()) y = -y;
+  }
+  return q;
 }
 
 // 16-byte staging of consecutive line pairs (lines are produced strictly in
@@ -123,7 +222,8 @@ struct LineWriter {
 
 // MPEG-1 long-block scale factors (maindata.go:233-279): parts in `read` are
 // read from the stream, parts in `store` are written to sfl.
-MP3G_HD_INLINE void sf_mpeg1_long(Reader& r, int slen1, int slen2, uint32_t read, uint32_t store,
+template <bool kSwap>
+MP3G_HD_INLINE void sf_mpeg1_long(Reader<kSwap>& r, int slen1, int slen2, uint32_t read, uint32_t store,
                                               uint8_t* sfl) {
 #pragma unroll
   for (int part = 0; part < 4; part++) {
@@ -139,11 +239,18 @@ MP3G_HD_INLINE void sf_mpeg1_long(Reader& r, int slen1, int slen2, uint32_t read
   }
 }
 
+// The 64-bit-aligned bit position the job's reads start from (granule 0's
+// part 2 for an scfsi copy).
+MP3G_HD_INLINE uint64_t job_base(const mp3g_hjob& J) { return (J.part2_start - J.scf0_delta) & ~63ull; }
+
 // Decodes job j (= 2 * granule + channel): scale factors and count1 into
-// gran[j / 2].ch[j % 2], the 576 lines into coef[j * 576 ..].  T / s_root /
-// s_lin: the HuffLut entries, roots and linbits (LDS on the device).
-MP3G_HD_INLINE void decode_job(const mp3g_hjob& job, uint64_t j, const uint8_t* md, mp3g_granule* gran,
-                               int16_t* coef, const uint32_t* T, const uint32_t* s_root, const uint32_t* s_lin) {
+// gran[j / 2].ch[j % 2], the 576 lines into coef[j * 576 ..].  words / nw: the
+// main data from job_base(job) on (Reader); T / s_root / s_lin: the HuffLut
+// entries, roots and linbits (LDS on the device).
+template <bool kSwap>
+MP3G_HD_INLINE void decode_job(const mp3g_hjob& job, uint64_t j, const uint64_t* words, uint32_t nw,
+                               mp3g_granule* gran, int16_t* coef, const uint32_t* T, const uint32_t* s_root,
+                               const uint32_t* s_lin) {
   // a register copy: the coefficient / scale-factor stores below could alias
   // the job in the compiler's eyes, which would re-load its fields from memory
   // (with a full vmcnt wait) in every loop iteration
@@ -158,9 +265,10 @@ MP3G_HD_INLINE void decode_job(const mp3g_hjob& job, uint64_t j, const uint8_t* 
   uint8_t* sfl = C.scalefac_l;
   uint8_t* sfs = &C.scalefac_s[0][0];
 
-  const uint64_t base = (J.part2_start - J.scf0_delta) & ~31ull;
-  Reader r;
-  r.w = reinterpret_cast<const uint32_t*>(md + (base >> 3));
+  const uint64_t base = job_base(J);
+  Reader<kSwap> r;
+  r.w = words;
+  r.nw = nw;
   r.end = J.bit_end > base ? (uint32_t)(J.bit_end - base) : 0u;
   const uint32_t part2 = (uint32_t)(J.part2_start - base);
 
@@ -225,30 +333,21 @@ MP3G_HD_INLINE void decode_job(const mp3g_hjob& job, uint64_t j, const uint8_t* 
     const uint32_t pend = part2 + p23 - 1;  // bitPosEnd
     const int bv2 = 2 * (int)J.big_values;  // <= 576 (the scan rejects more)
     const int r1 = J.region1_start, r2 = J.region2_start;
+    const uint32_t root0 = s_root[J.table_select[0]], root1 = s_root[J.table_select[1]],
+                   root2 = s_root[J.table_select[2]];
+    const int lb0 = (int)s_lin[J.table_select[0]], lb1 = (int)s_lin[J.table_select[1]],
+              lb2 = (int)s_lin[J.table_select[2]];
     for (; i < bv2; i += 2) {
-      const int tbl = i < r1 ? J.table_select[0] : i < r2 ? J.table_select[1] : J.table_select[2];
-      const uint32_t root = s_root[tbl];
+      const uint32_t root = i < r1 ? root0 : i < r2 ? root1 : root2;
+      const int lb = i < r1 ? lb0 : i < r2 ? lb1 : lb2;
       int x = 0, y = 0;
-      if (root) {
-        const uint32_t xy = decode_xy(r, T, root);
-        x = (int)(xy >> 4);
-        y = (int)(xy & 15u);
-        const int lb = (int)s_lin[tbl];
-        if (lb && x == 15) x += (int)r.bits(lb);
-        if (x && r.bit()) x = -x;
-        if (lb && y == 15) y += (int)r.bits(lb);
-        if (y && r.bit()) y = -y;
-      }
+      if (root) decode_pair(r, T, root, lb, x, y);
       out.put(i, x, y);
     }
     const uint32_t qroot = s_root[32 + J.count1_table];
     while (i <= 572 && r.pos <= pend) {
-      const uint32_t q = decode_xy(r, T, qroot) & 15u;
-      int v = (int)((q >> 3) & 1u), w = (int)((q >> 2) & 1u), x = (int)((q >> 1) & 1u), y = (int)(q & 1u);
-      if (v && r.bit()) v = -v;
-      if (w && r.bit()) w = -w;
-      if (x && r.bit()) x = -x;
-      if (y && r.bit()) y = -y;
+      int v, w, x, y;
+      decode_quad(r, T, qroot, v, w, x, y);
       out.put(i, v, w);
       out.put(i + 2, x, y);
       i += 4;
@@ -259,6 +358,16 @@ MP3G_HD_INLINE void decode_job(const mp3g_hjob& job, uint64_t j, const uint8_t* 
   out.finish(i);
   for (int k = count1; k < i; k++) row[k] = 0;  // lines the overrun check removed
   C.count1 = (uint16_t)count1;
+}
+
+// decode_job straight from the main data in memory (stream byte order; must
+// be 8-byte aligned and readable up to 8 bytes past the last bit_end).
+MP3G_HD_INLINE void decode_job_direct(const mp3g_hjob& job, uint64_t j, const uint8_t* md, mp3g_granule* gran,
+                                      int16_t* coef, const uint32_t* T, const uint32_t* s_root,
+                                      const uint32_t* s_lin) {
+  const uint64_t base = job_base(job);
+  const uint32_t nw = job.bit_end > base ? (uint32_t)((job.bit_end - base + 63) >> 6) : 0u;
+  decode_job<true>(job, j, reinterpret_cast<const uint64_t*>(md + (base >> 3)), nw, gran, coef, T, s_root, s_lin);
 }
 
 }  // namespace huff

@@ -85,6 +85,7 @@ def hjob_host(tmp_path_factory):
                            os.path.join(REPO, "go-mp3_amd", "csrc", "huff_lut.cpp")])
     L = C.CDLL(str(out))
     L.hjob_decode_host.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p]
+    L.hjob_decode_host_staged.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]
     return L
 
 
@@ -98,12 +99,17 @@ def check_against_parse(hjob_host, datas, what):
     jobs = s["jobs"]
     assert ((jobs["sf_kind"][1::2] == 0) == (((s["granules"]["header"] >> 6) & 3) == 3)).all()
     assert (jobs["big_values"][jobs["part2_3_length"] > 0] <= 288).all()
-    g = s["granules"].copy()
-    c = np.full((n, 2, 576), 0x5A5A, np.int16)  # poison: every line must be written
-    assert hjob_host.hjob_decode_host(jobs.ctypes.data, n, s["main_data"].ctypes.data, g.ctypes.data,
-                                      c.ctypes.data) == 0
-    assert g.tobytes() == g2.tobytes(), f"{what}: descriptors differ"
-    assert np.array_equal(c, c2), f"{what}: coefficients differ"
+    # direct reads, then the kernel's LDS staging (960 words as on the
+    # device, and a tiny buffer so that groups also take the direct path)
+    for stage_words in (None, 960, 64):
+        g = s["granules"].copy()
+        c = np.full((n, 2, 576), 0x5A5A, np.int16)  # poison: every line must be written
+        args = (jobs.ctypes.data, n, s["main_data"].ctypes.data, g.ctypes.data, c.ctypes.data)
+        rc = hjob_host.hjob_decode_host(*args) if stage_words is None else \
+            hjob_host.hjob_decode_host_staged(*args, stage_words)
+        assert rc == 0
+        assert g.tobytes() == g2.tobytes(), f"{what} (stage {stage_words}): descriptors differ"
+        assert np.array_equal(c, c2), f"{what} (stage {stage_words}): coefficients differ"
 
 
 def test_jobs_sample_files(hjob_host, sample_files):
