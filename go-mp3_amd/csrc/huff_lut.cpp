@@ -12,7 +12,7 @@ namespace {
 struct Code {
   uint32_t code;
   int len;
-  uint32_t val;  // x << 4 | y
+  uint32_t val;  // the leaf's value bits (huff_lut.h)
 };
 
 struct Builder {
@@ -39,7 +39,7 @@ struct Builder {
       const uint32_t bits = c.code & ((1u << rem) - 1u);  // the code's bits after `depth`
       if (rem <= w) {
         const uint32_t first = bits << (w - rem);
-        for (uint32_t i = 0; i < (1u << (w - rem)); i++) t->e[off + first + i] = ((uint32_t)c.len << 8) | c.val;
+        for (uint32_t i = 0; i < (1u << (w - rem)); i++) t->e[off + first + i] = (uint16_t)(((uint32_t)c.len << 8) | c.val);
       } else {
         sub[bits >> (rem - w)].push_back(c);
       }
@@ -49,7 +49,11 @@ struct Builder {
       int cw = 0;
       const uint32_t child = block(sub[i], depth + w, 6, &cw);
       if (!ok) return 0;
-      t->e[off + i] = 0x80000000u | ((uint32_t)cw << 24) | child;
+      if ((child & 1u) || (child >> 1) > 0xfffu) {
+        ok = false;
+        return 0;
+      }
+      t->e[off + i] = (uint16_t)(0x8000u | ((uint32_t)cw << 12) | (child >> 1));
     }
     return off;
   }
@@ -65,8 +69,14 @@ bool build_huff_lut(HuffLut* t) {
   for (int tree = 0; tree < 34; tree++) {
     std::vector<Code> cs;
     for (int k = 0; k < HUFF_N_CODES; k++)
-      if (HUFF_CODES[k].tree == tree)
-        cs.push_back({HUFF_CODES[k].code, HUFF_CODES[k].len, (uint32_t)((HUFF_CODES[k].x << 4) | HUFF_CODES[k].y)});
+      if (HUFF_CODES[k].tree == tree) {
+        const uint32_t x = HUFF_CODES[k].x, y = HUFF_CODES[k].y;
+        // count1 trees code vwxy in y: a = v, b = w, c = x, d = y
+        const uint32_t val = tree >= 32 ? ((y >> 3) & 1u) << 4 | ((y >> 2) & 1u) | ((y >> 1) & 1u) << 13 |
+                                              (y & 1u) << 14
+                                        : x << 4 | y;
+        cs.push_back({HUFF_CODES[k].code, HUFF_CODES[k].len, val});
+      }
     if (cs.empty()) continue;
     int w0 = 0;
     const uint32_t off = b.block(cs, 0, 8, &w0);
@@ -77,9 +87,15 @@ bool build_huff_lut(HuffLut* t) {
   // complete prefix codes: every entry is a leaf (len >= 1) or a link
   for (uint32_t i = 0; i < b.n; i++)
     if (t->e[i] == 0) return false;
+  // tables that code nothing (0, 4, 14) point at a 1-bit block of two
+  // zero-length x = y = 0 leaves: decoding them reads nothing, branch-free
+  if (b.n + 2 > (uint32_t)kHuffMaxEntries) return false;
+  const uint32_t null_root = b.n | (1u << 24);
+  t->e[b.n] = t->e[b.n + 1] = 0;
+  b.n += 2;
   for (int table = 0; table < 34; table++) {
     const int tree = HUFF_TABLE_TREE[table];
-    t->root[table] = tree >= 0 && have[tree] ? tree_root[tree] : 0u;
+    t->root[table] = tree >= 0 && have[tree] ? tree_root[tree] : null_root;
     t->linbits[table] = (uint32_t)HUFF_TABLE_LINBITS[table];
   }
   t->n_entries = b.n;

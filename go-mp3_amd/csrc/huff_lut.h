@@ -3,13 +3,16 @@
 // codeword lists (huffman_codes.inc; table directory of reference
 // internal/huffman/huffman.go:311-346) and uploaded once per device.
 //
-// Every tree is a multi-level table of 32-bit entries: the root block is
+// Every tree is a multi-level table of 16-bit entries: the root block is
 // indexed by the next w0 bits of the stream (w0 = min(longest codeword, 8)),
 // each deeper block by the next w bits (w = min(remaining length, 6)).
-//   leaf : bit 31 = 0, bits 8..12 = codeword length, bits 0..7 = x << 4 | y
-//          (count1 trees 32/33: x = 0, y = vwxy)
-//   link : bit 31 = 1, bits 24..27 = width of the next block, bits 0..23 =
-//          its first entry
+//   leaf : bit 15 = 0, bits 8..12 = codeword length, bits 4..7 = a, 0..3 = b,
+//          bit 13 = c, bit 14 = d.  Big-value trees: (a, b) = (x, y), c = d =
+//          0; count1 trees 32/33: (a, b, c, d) = (v, w, x, y).  The decoder
+//          then reads, for a, b, c, d in turn, the linbits of a 15 and the
+//          sign of a non-zero value: one code path for both regions.
+//   link : bit 15 = 1, bits 12..14 = width of the next block, bits 0..11 =
+//          its first entry / 2 (blocks are >= 2 entries, so offsets are even)
 // The builder checks that every entry is filled (the trees are complete
 // prefix codes), so a lookup cannot fail: huffman.Decode's error return
 // (huffman.go:382-386) is unreachable for bitstream input, as for the host
@@ -19,15 +22,16 @@
 
 namespace mp3g {
 
-constexpr int kHuffMaxEntries = 4608;  // 4,504 used (18 KB of LDS)
+constexpr int kHuffMaxEntries = 4608;  // 4,506 used (9 KB of LDS)
 struct HuffLut {
-  // per table 0..33: root block offset | w0 << 24; 0 = the table codes
-  // nothing (tables 0, 4, 14: huffman.go:354-356)
+  // per table 0..33: root block offset | w0 << 24.  Tables that code
+  // nothing (0, 4, 14: huffman.go:354-356) share a block of zero-length
+  // x = y = 0 leaves.
   uint32_t root[34];
   uint32_t linbits[34];
   uint32_t n_entries;
   uint32_t pad[3];
-  uint32_t e[kHuffMaxEntries];
+  uint16_t e[kHuffMaxEntries];
 };
 
 // Builds the tables; returns false if they do not fit or a tree is incomplete.

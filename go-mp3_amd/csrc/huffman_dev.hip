@@ -11,7 +11,7 @@
 // 8-byte loads (byte-swapped once), so the bit-serial loop never waits on
 // global memory (on gfx9 a load's vmcnt wait would also wait for the
 // coefficient stores issued before it).  The Huffman tables (huff_lut.h,
-// 18 KB) live in LDS too.
+// 9 KB) live in LDS too.
 // (compiled as part of kernels.hip)
 #include "huffman_job.h"
 
@@ -21,10 +21,13 @@ namespace huff {
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
 // Main data staged per wave: 64 consecutive jobs (16 MPEG-1 stereo frames)
-// span ~6.1 KB at 128 kbps.  7.5 KB per wave keeps the block at 48 KB of
-// LDS (3 blocks = 12 waves per CU); a wave whose span does not fit reads
-// straight from global memory.
-constexpr int kStageWords = 960;
+// span ~6.1 KB at 128 kbps.  7.5 KB per wave + the 9 KB of tables keep the
+// block under 40 KB of LDS (4 blocks = 16 waves per CU); a wave whose span
+// does not fit reads straight from global memory.
+#ifndef MP3G_HUFF_STAGE_WORDS
+#define MP3G_HUFF_STAGE_WORDS 960
+#endif
+constexpr int kStageWords = MP3G_HUFF_STAGE_WORDS;  // 0: no staging (experiments)
 
 __device__ __forceinline__ uint64_t wave_min(uint64_t v) {
   for (int o = 32; o; o >>= 1) {
@@ -44,11 +47,14 @@ __device__ __forceinline__ uint64_t wave_max(uint64_t v) {
 __global__ void __launch_bounds__(kThreads)
 huffman_kernel(const mp3g_hjob* __restrict__ jobs, uint64_t n_jobs, const uint8_t* __restrict__ md,
                mp3g_granule* __restrict__ gran, int16_t* __restrict__ coef) {
-  __shared__ uint32_t T[kHuffMaxEntries];
+  __shared__ uint32_t T2[kHuffMaxEntries / 2];  // the 16-bit entries, two per word
   __shared__ uint32_t s_root[34], s_lin[34];
-  __shared__ uint64_t stage[kWaves][kStageWords];
-  const uint32_t n_e = g_huff.n_entries;
-  for (uint32_t i = threadIdx.x; i < n_e; i += kThreads) T[i] = g_huff.e[i];
+  // + 4 words: the LDS reader loads up to 3 words past a job's last word
+  __shared__ uint64_t stage[kWaves][kStageWords ? kStageWords + 4 : 1];
+  const uint32_t n_w = (g_huff.n_entries + 1) / 2;
+  const uint32_t* src_e = reinterpret_cast<const uint32_t*>(g_huff.e);
+  for (uint32_t i = threadIdx.x; i < n_w; i += kThreads) T2[i] = src_e[i];
+  const uint16_t* T = reinterpret_cast<const uint16_t*>(T2);
   if (threadIdx.x < 34) {
     s_root[threadIdx.x] = g_huff.root[threadIdx.x];
     s_lin[threadIdx.x] = g_huff.linbits[threadIdx.x];
@@ -63,7 +69,7 @@ huffman_kernel(const mp3g_hjob* __restrict__ jobs, uint64_t n_jobs, const uint8_
   const uint64_t lo = wave_min(reads ? base : ~0ull);
   const uint64_t hi = wave_max(reads ? J.bit_end : 0ull);
   const uint64_t nwords = hi > lo && lo != ~0ull ? ((hi - lo + 63) >> 6) : 0ull;
-  const bool staged = nwords <= (uint64_t)kStageWords;  // wave-uniform
+  const bool staged = kStageWords && nwords <= (uint64_t)kStageWords;  // wave-uniform
   const int wv = threadIdx.x >> 6;
   if (staged) {
     const uint64_t* src = reinterpret_cast<const uint64_t*>(md + (lo >> 3));

@@ -45,7 +45,13 @@ struct Reader {
   uint64_t nxt;   // bits [wpos + 64, wpos + 128)
   uint64_t nn;    // the stored word of bits [wpos + 128, wpos + 192), in flight
 
-  MP3G_HD_INLINE uint64_t load(uint32_t k) const { return k < nw ? w[k] : 0ull; }
+  // kSwap (memory): nothing at or past word nw is loaded.  LDS staging: the
+  // buffer holds 3 words past nw (huffman_dev.hip) and bits past `end` never
+  // reach a result, so the load is unconditional, only clamped to the buffer
+  // (a corrupt stream's part 2 may start past its end).
+  MP3G_HD_INLINE uint64_t load(uint32_t k) const {
+    return kSwap ? (k < nw ? w[k] : 0ull) : w[k < nw + 3u ? k : nw + 3u];
+  }
   MP3G_HD_INLINE static uint64_t order(uint64_t raw) { return kSwap ? bswap64(raw) : raw; }
   MP3G_HD_INLINE void seek(uint32_t p) {
     pos = p;
@@ -58,11 +64,20 @@ struct Reader {
   // last call.  The next word is loaded two words ahead, so its latency
   // overlaps ~64 bits of decoding.
   MP3G_HD_INLINE void refill() {
-    if (pos - wpos >= 64u) {
-      win = nxt;
-      nxt = order(nn);
-      wpos += 64;
-      nn = load((wpos >> 6) + 2);
+    if (kSwap) {
+      if (pos - wpos >= 64u) {
+        win = nxt;
+        nxt = order(nn);
+        wpos += 64;
+        nn = load((wpos >> 6) + 2);
+      }
+    } else {  // LDS: branch-free, the next word is read every time
+      const bool adv = pos - wpos >= 64u;
+      const uint64_t n3 = load((wpos >> 6) + 3);
+      win = adv ? nxt : win;
+      nxt = adv ? nn : nxt;
+      nn = adv ? n3 : nn;
+      wpos += adv ? 64u : 0u;
     }
   }
   // the 64 stream bits from pos (not masked at the end)
@@ -94,106 +109,93 @@ struct Reader {
   }
 };
 
-// The leaf the 32 stream bits `p` reach in the table at `root`; *len = its
-// codeword length.
-MP3G_HD_INLINE uint32_t lut_leaf(const uint32_t* T, uint32_t root, uint32_t p, uint32_t* len) {
+// The leaf the 32 stream bits `p` reach in the table at `root` (huff_lut.h);
+// *len = its codeword length.
+MP3G_HD_INLINE uint32_t lut_leaf(const uint16_t* T, uint32_t root, uint32_t p, uint32_t* len) {
   int used = (int)(root >> 24);
   uint32_t e = T[(root & 0xffffffu) + (p >> (32 - used))];
-  while (e & 0x80000000u) {
-    const int wd = (int)((e >> 24) & 15u);
-    e = T[(e & 0xffffffu) + ((p << used) >> (32 - wd))];
+  while (e & 0x8000u) {
+    const int wd = (int)((e >> 12) & 7u);
+    e = T[((e & 0xfffu) << 1) + ((p << used) >> (32 - wd))];
     used += wd;
   }
   *len = (e >> 8) & 31u;
-  return e & 255u;
+  return e;
 }
 
 // huffman.Decode's tree walk near the end of the buffer: the leaf the next
 // bits reach (zeros past the end) and the advance of its Bit() calls,
 // min(len, end - pos).
 template <bool kSwap>
-MP3G_HD_INLINE uint32_t decode_xy(Reader<kSwap>& r, const uint32_t* T, uint32_t root) {
+MP3G_HD_INLINE uint32_t decode_xy(Reader<kSwap>& r, const uint16_t* T, uint32_t root) {
   r.refill();
   uint32_t len;
-  const uint32_t xy = lut_leaf(T, root, (uint32_t)(r.peek64m() >> 32), &len);
+  const uint32_t e = lut_leaf(T, root, (uint32_t)(r.peek64m() >> 32), &len);
   if (r.pos < r.end) r.pos = r.pos + len < r.end ? r.pos + len : r.end;
-  return xy;
+  return e;
 }
 
-// One big-values pair (maindata/huffman.go:66-104): codeword, x linbits,
-// x sign, y linbits, y sign.  Far from the end (<= 19 + 2 * 14 = 47 bits to
-// go) every field comes out of one 64-bit peek; otherwise each read follows
-// the reference's clamping.
+// One symbol: a big-values pair (maindata/huffman.go:66-104: codeword, x
+// linbits, x sign, y linbits, y sign) or a count1 quad (huffman.go:106-131:
+// codeword, v w x y signs), in one code path (lb = 0 for quads, c = d = 0 for
+// pairs: huff_lut.h).  Far from the end (<= 19 + 2 * 14 = 47 bits to go)
+// every field comes out of one 64-bit peek; otherwise each read follows the
+// reference's clamping.
 template <bool kSwap>
-MP3G_HD_INLINE void decode_pair(Reader<kSwap>& r, const uint32_t* T, uint32_t root, int lb, int& xo, int& yo) {
+MP3G_HD_INLINE void decode_sym(Reader<kSwap>& r, const uint16_t* T, uint32_t root, uint32_t lb, int& ao, int& bo,
+                               int& co, int& dox) {
   r.refill();
-  int x, y;
+  int a, b, c, d;
   if (r.pos + 47u <= r.end) {
     const uint64_t p64 = r.peek64();
     uint32_t len;
-    const uint32_t xy = lut_leaf(T, root, (uint32_t)(p64 >> 32), &len);
-    x = (int)(xy >> 4);
-    y = (int)(xy & 15u);
-    const uint32_t q = (uint32_t)((p64 << len) >> 32);  // the <= 28 bits after the codeword
-    const int lbs = lb ? lb : 1;
-    uint32_t o = 0;
-    if (lb && x == 15) {
-      x += (int)(q >> (32 - lbs));
-      o = (uint32_t)lb;
-    }
-    if (x) {
-      x = ((q << o) >> 31) ? -x : x;
-      o++;
-    }
-    if (lb && y == 15) {
-      y += (int)((q << o) >> (32 - lbs));
-      o += (uint32_t)lb;
-    }
-    if (y) {
-      y = ((q << o) >> 31) ? -y : y;
-      o++;
-    }
-    r.pos += len + o;
+    const uint32_t e = lut_leaf(T, root, (uint32_t)(p64 >> 32), &len);
+    a = (int)((e >> 4) & 15u);
+    b = (int)(e & 15u);
+    c = (int)((e >> 13) & 1u);
+    d = (int)((e >> 14) & 1u);
+    uint32_t q = (uint32_t)((p64 << len) >> 32);  // the <= 28 bits after the codeword
+    uint32_t o = len;
+    // a: linbits of a 15, then the sign of a non-zero value; the same for b
+    const uint32_t na = a == 15 ? lb : 0u;
+    a += (int)((q >> 1) >> (31u - na));
+    const uint32_t sa = a ? 1u : 0u;
+    const bool nega = (q << na) & (sa << 31);
+    q <<= na + sa;
+    o += na + sa;
+    const uint32_t nb = b == 15 ? lb : 0u;
+    b += (int)((q >> 1) >> (31u - nb));
+    const uint32_t sb = b ? 1u : 0u;
+    const bool negb = (q << nb) & (sb << 31);
+    q <<= nb + sb;
+    o += nb + sb;
+    // c, d: quads only (0 / 1, no linbits)
+    const bool negc = c && (q >> 31);
+    q <<= (uint32_t)c;
+    const bool negd = d && (q >> 31);
+    o += (uint32_t)(c + d);
+    a = nega ? -a : a;
+    b = negb ? -b : b;
+    c = negc ? -c : c;
+    d = negd ? -d : d;
+    r.pos += o;
   } else {
-    const uint32_t xy = decode_xy(r, T, root);
-    x = (int)(xy >> 4);
-    y = (int)(xy & 15u);
-    if (lb && x == 15) x += (int)r.bits(lb);
-    if (x && r.bit()) x = -x;
-    if (lb && y == 15) y += (int)r.bits(lb);
-    if (y && r.bit()) y = -y;
+    const uint32_t e = decode_xy(r, T, root);
+    a = (int)((e >> 4) & 15u);
+    b = (int)(e & 15u);
+    c = (int)((e >> 13) & 1u);
+    d = (int)((e >> 14) & 1u);
+    if (lb && a == 15) a += (int)r.bits((int)lb);
+    if (a && r.bit()) a = -a;
+    if (lb && b == 15) b += (int)r.bits((int)lb);
+    if (b && r.bit()) b = -b;
+    if (c && r.bit()) c = -c;
+    if (d && r.bit()) d = -d;
   }
-  xo = x;
-  yo = y;
-}
-
-// One count1 quad (maindata/huffman.go:106-131): codeword <= 6 bits + 4 signs.
-template <bool kSwap>
-MP3G_HD_INLINE uint32_t decode_quad(Reader<kSwap>& r, const uint32_t* T, uint32_t root, int& v, int& w, int& x,
-                                    int& y) {
-  r.refill();
-  uint32_t q;
-  if (r.pos + 10u <= r.end) {
-    const uint64_t p64 = r.peek64();
-    uint32_t len;
-    q = lut_leaf(T, root, (uint32_t)(p64 >> 32), &len) & 15u;
-    const uint32_t s = (uint32_t)((p64 << len) >> 32);
-    v = (int)((q >> 3) & 1u), w = (int)((q >> 2) & 1u), x = (int)((q >> 1) & 1u), y = (int)(q & 1u);
-    uint32_t o = 0;
-    if (v) v = ((s << o++) >> 31) ? -1 : 1;
-    if (w) w = ((s << o++) >> 31) ? -1 : 1;
-    if (x) x = ((s << o++) >> 31) ? -1 : 1;
-    if (y) y = ((s << o++) >> 31) ? -1 : 1;
-    r.pos += len + o;
-  } else {
-    q = decode_xy(r, T, root) & 15u;
-    v = (int)((q >> 3) & 1u), w = (int)((q >> 2) & 1u), x = (int)((q >> 1) & 1u), y = (int)(q & 1u);
-    if (v && r.bit()) v = -v;
-    if (w && r.bit()) w = -w;
-    if (x && r.bit()) x = -x;
-    if (y && r.bit()) y = -y;
-  }
-  return q;
+  ao = a;
+  bo = b;
+  co = c;
+  dox = d;
 }
 
 // 16-byte staging of consecutive line pairs (lines are produced strictly in
@@ -249,7 +251,7 @@ MP3G_HD_INLINE uint64_t job_base(const mp3g_hjob& J) { return (J.part2_start - J
 // entries, roots and linbits (LDS on the device).
 template <bool kSwap>
 MP3G_HD_INLINE void decode_job(const mp3g_hjob& job, uint64_t j, const uint64_t* words, uint32_t nw,
-                               mp3g_granule* gran, int16_t* coef, const uint32_t* T, const uint32_t* s_root,
+                               mp3g_granule* gran, int16_t* coef, const uint16_t* T, const uint32_t* s_root,
                                const uint32_t* s_lin) {
   // a register copy: the coefficient / scale-factor stores below could alias
   // the job in the compiler's eyes, which would re-load its fields from memory
@@ -334,22 +336,20 @@ MP3G_HD_INLINE void decode_job(const mp3g_hjob& job, uint64_t j, const uint64_t*
     const int bv2 = 2 * (int)J.big_values;  // <= 576 (the scan rejects more)
     const int r1 = J.region1_start, r2 = J.region2_start;
     const uint32_t root0 = s_root[J.table_select[0]], root1 = s_root[J.table_select[1]],
-                   root2 = s_root[J.table_select[2]];
-    const int lb0 = (int)s_lin[J.table_select[0]], lb1 = (int)s_lin[J.table_select[1]],
-              lb2 = (int)s_lin[J.table_select[2]];
+                   root2 = s_root[J.table_select[2]], qroot = s_root[32 + J.count1_table];
+    const uint32_t lb0 = s_lin[J.table_select[0]], lb1 = s_lin[J.table_select[1]], lb2 = s_lin[J.table_select[2]];
     for (; i < bv2; i += 2) {
       const uint32_t root = i < r1 ? root0 : i < r2 ? root1 : root2;
-      const int lb = i < r1 ? lb0 : i < r2 ? lb1 : lb2;
-      int x = 0, y = 0;
-      if (root) decode_pair(r, T, root, lb, x, y);
-      out.put(i, x, y);
+      const uint32_t lb = i < r1 ? lb0 : i < r2 ? lb1 : lb2;
+      int a, b, c, d;
+      decode_sym(r, T, root, lb, a, b, c, d);
+      out.put(i, a, b);
     }
-    const uint32_t qroot = s_root[32 + J.count1_table];
     while (i <= 572 && r.pos <= pend) {
-      int v, w, x, y;
-      decode_quad(r, T, qroot, v, w, x, y);
-      out.put(i, v, w);
-      out.put(i + 2, x, y);
+      int a, b, c, d;
+      decode_sym(r, T, qroot, 0u, a, b, c, d);
+      out.put(i, a, b);
+      out.put(i + 2, c, d);
       i += 4;
     }
     count1 = i;
@@ -363,7 +363,7 @@ MP3G_HD_INLINE void decode_job(const mp3g_hjob& job, uint64_t j, const uint64_t*
 // decode_job straight from the main data in memory (stream byte order; must
 // be 8-byte aligned and readable up to 8 bytes past the last bit_end).
 MP3G_HD_INLINE void decode_job_direct(const mp3g_hjob& job, uint64_t j, const uint8_t* md, mp3g_granule* gran,
-                                      int16_t* coef, const uint32_t* T, const uint32_t* s_root,
+                                      int16_t* coef, const uint16_t* T, const uint32_t* s_root,
                                       const uint32_t* s_lin) {
   const uint64_t base = job_base(job);
   const uint32_t nw = job.bit_end > base ? (uint32_t)((job.bit_end - base + 63) >> 6) : 0u;

@@ -53,7 +53,8 @@ _lib = None
 
 
 def lib_path():
-    return os.path.join(HERE, "libmp3g.so")
+    # MP3G_LIB: another build of the same library (kernel experiments)
+    return os.environ.get("MP3G_LIB") or os.path.join(HERE, "libmp3g.so")
 
 
 def lib():

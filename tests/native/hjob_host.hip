@@ -26,7 +26,7 @@ extern "C" int hjob_decode_host_staged(const mp3g_hjob* jobs, uint64_t n_granule
   static const bool ok = mp3g::build_huff_lut(&lut);
   if (!ok) return 1;
   const uint64_t n = 2 * n_granules;
-  std::vector<uint64_t> stage(stage_words);
+  std::vector<uint64_t> stage(stage_words + 4);  // the reader loads up to 3 words past nw
   for (uint64_t j0 = 0; j0 < n; j0 += 64) {
     const uint64_t j1 = j0 + 64 < n ? j0 + 64 : n;
     uint64_t lo = ~0ull, hi = 0;
