@@ -76,12 +76,25 @@ huffman_kernel(const mp3g_hjob* __restrict__ jobs, uint64_t n_jobs, const uint8_
     for (uint32_t k = threadIdx.x & 63; k < (uint32_t)nwords; k += 64) stage[wv][k] = bswap64(src[k]);
   }
   __syncthreads();
-  if (!valid) return;
-  if (staged) {
-    const uint32_t off = reads ? (uint32_t)((base - lo) >> 6) : 0u;
-    decode_job<false>(J, j, &stage[wv][off], (uint32_t)nwords - off, gran, coef, T, s_root, s_lin);
-  } else {
-    decode_job_direct(J, j, md, gran, coef, T, s_root, s_lin);
+  int z = MP3G_LINES;  // first line this lane's row still needs zeroed
+  if (valid) {
+    if (staged) {
+      const uint32_t off = reads ? (uint32_t)((base - lo) >> 6) : 0u;
+      z = decode_job<false>(J, j, &stage[wv][off], (uint32_t)nwords - off, gran, coef, T, s_root, s_lin);
+    } else {
+      z = decode_job_direct(J, j, md, gran, coef, T, s_root, s_lin);
+    }
+  }
+  // zero tails of the wave's 64 rows (consecutive jobs), one row at a time
+  // with the whole wave: contiguous 16-B slots instead of a burst of
+  // scattered per-lane stores at the end of every job
+  const int lane = threadIdx.x & 63;
+  const uint64_t j0 = j - (uint64_t)lane;
+  for (int rr = 0; rr < 64; rr++) {
+    const int zr = __shfl(z, rr, 64);
+    if (zr >= MP3G_LINES) continue;  // wave-uniform
+    uint4* row = reinterpret_cast<uint4*>(coef + (j0 + rr) * MP3G_LINES);
+    for (int s8 = (zr >> 3) + lane; s8 < MP3G_LINES / 8; s8 += 64) row[s8] = make_uint4(0u, 0u, 0u, 0u);
   }
 }
 

@@ -215,18 +215,35 @@ struct LineWriter {
       b0 = b1 = b2 = b3 = 0u;
     }
   }
-  // flushes the pending block; lines [i, 576) zero (i even)
-  MP3G_HD_INLINE void finish(int i) {
+  // flushes the pending block (lines up to i, i even, then zeros to the next
+  // multiple of 8); returns that multiple of 8: the first line of the row
+  // left for the zero fill
+  MP3G_HD_INLINE int finish(int i) {
     if (i & 7) *reinterpret_cast<uint4*>(row + (i & ~7)) = make_uint4(b0, b1, b2, b3);
-    for (int k = (i + 7) & ~7; k < 576; k += 8) *reinterpret_cast<uint4*>(row + k) = make_uint4(0u, 0u, 0u, 0u);
+    return (i + 7) & ~7;
   }
+};
+
+// lines [z, 576) of a row = 0 (z a multiple of 8): one lane's own stores,
+// for the host build; the kernel zero-fills a wave's rows together
+// (huffman_dev.hip), so the tail of a job is not 72 scattered stores
+MP3G_HD_INLINE void zero_fill_row(int16_t* row, int z) {
+  for (int k = z; k < MP3G_LINES; k += 8) *reinterpret_cast<uint4*>(row + k) = make_uint4(0u, 0u, 0u, 0u);
+}
+
+// Scale-factor destination: scalefac_l[22] / scalefac_s[13][3] of the channel.
+struct SfSink {
+  uint8_t* l;
+  uint8_t* s;
+  MP3G_HD_INLINE void put_l(int k, uint32_t v) { l[k] = (uint8_t)v; }
+  MP3G_HD_INLINE void put_s(int k, uint32_t v) { s[k] = (uint8_t)v; }
 };
 
 // MPEG-1 long-block scale factors (maindata.go:233-279): parts in `read` are
 // read from the stream, parts in `store` are written to sfl.
 template <bool kSwap>
 MP3G_HD_INLINE void sf_mpeg1_long(Reader<kSwap>& r, int slen1, int slen2, uint32_t read, uint32_t store,
-                                              uint8_t* sfl) {
+                                              SfSink& sf) {
 #pragma unroll
   for (int part = 0; part < 4; part++) {
     if (!((read >> part) & 1u)) continue;
@@ -236,7 +253,7 @@ MP3G_HD_INLINE void sf_mpeg1_long(Reader<kSwap>& r, int slen1, int slen2, uint32
     const bool st = (store >> part) & 1u;
     for (int sfb = lo; sfb < hi; sfb++) {
       const uint32_t v = nb ? r.bits(nb) : 0u;
-      if (st) sfl[sfb] = (uint8_t)v;
+      if (st) sf.put_l(sfb, v);
     }
   }
 }
@@ -246,11 +263,13 @@ MP3G_HD_INLINE void sf_mpeg1_long(Reader<kSwap>& r, int slen1, int slen2, uint32
 MP3G_HD_INLINE uint64_t job_base(const mp3g_hjob& J) { return (J.part2_start - J.scf0_delta) & ~63ull; }
 
 // Decodes job j (= 2 * granule + channel): scale factors and count1 into
-// gran[j / 2].ch[j % 2], the 576 lines into coef[j * 576 ..].  words / nw: the
-// main data from job_base(job) on (Reader); T / s_root / s_lin: the HuffLut
-// entries, roots and linbits (LDS on the device).
+// gran[j / 2].ch[j % 2], the 576 lines into coef[j * 576 ..] up to the
+// returned line z (a multiple of 8); lines [z, 576) are left for the caller
+// to zero (zero_fill_row).  words / nw: the main data from job_base(job) on
+// (Reader); T / s_root / s_lin: the HuffLut entries, roots and linbits (LDS
+// on the device).
 template <bool kSwap>
-MP3G_HD_INLINE void decode_job(const mp3g_hjob& job, uint64_t j, const uint64_t* words, uint32_t nw,
+MP3G_HD_INLINE int decode_job(const mp3g_hjob& job, uint64_t j, const uint64_t* words, uint32_t nw,
                                mp3g_granule* gran, int16_t* coef, const uint16_t* T, const uint32_t* s_root,
                                const uint32_t* s_lin) {
   // a register copy: the coefficient / scale-factor stores below could alias
@@ -260,12 +279,10 @@ MP3G_HD_INLINE void decode_job(const mp3g_hjob& job, uint64_t j, const uint64_t*
   int16_t* row = coef + j * MP3G_LINES;
   LineWriter out{row, 0u, 0u, 0u, 0u};
   if (J.sf_kind == MP3G_SF_NONE) {  // absent channel of a mono granule
-    out.finish(0);
-    return;
+    return 0;
   }
   mp3g_channel& C = gran[j >> 1].ch[j & 1];
-  uint8_t* sfl = C.scalefac_l;
-  uint8_t* sfs = &C.scalefac_s[0][0];
+  SfSink sf{C.scalefac_l, &C.scalefac_s[0][0]};
 
   const uint64_t base = job_base(J);
   Reader<kSwap> r;
@@ -283,29 +300,29 @@ MP3G_HD_INLINE void decode_job(const mp3g_hjob& job, uint64_t j, const uint64_t*
         // re-read them from granule 0's part 2 (zero where granule 0 has none)
         r.seek(part2 - J.scf0_delta);
         if (J.sf0_kind == MP3G_SF_MPEG1_LONG) {
-          sf_mpeg1_long(r, J.sf0_slen[0], J.sf0_slen[1], 15u, J.scfsi, sfl);
+          sf_mpeg1_long(r, J.sf0_slen[0], J.sf0_slen[1], 15u, J.scfsi, sf);
         } else if (J.sf0_kind == MP3G_SF_MPEG1_MIXED) {
           const int nb = J.sf0_slen[0];
           for (int sfb = 0; sfb < 8; sfb++) {
             const uint32_t v = nb ? r.bits(nb) : 0u;
-            if ((J.scfsi >> (sfb < 6 ? 0 : 1)) & 1u) sfl[sfb] = (uint8_t)v;
+            if ((J.scfsi >> (sfb < 6 ? 0 : 1)) & 1u) sf.put_l(sfb, v);
           }
         }
       }
       r.seek(part2);
-      sf_mpeg1_long(r, slen1, slen2, ~(uint32_t)J.scfsi & 15u, ~(uint32_t)J.scfsi & 15u, sfl);
+      sf_mpeg1_long(r, slen1, slen2, ~(uint32_t)J.scfsi & 15u, ~(uint32_t)J.scfsi & 15u, sf);
       break;
     case MP3G_SF_MPEG1_SHORT:
     case MP3G_SF_MPEG1_MIXED: {
       r.seek(part2);
       int s0 = 0;
       if (J.sf_kind == MP3G_SF_MPEG1_MIXED) {
-        for (int sfb = 0; sfb < 8; sfb++) sfl[sfb] = (uint8_t)(slen1 ? r.bits(slen1) : 0u);
+        for (int sfb = 0; sfb < 8; sfb++) sf.put_l(sfb, slen1 ? r.bits(slen1) : 0u);
         s0 = 3;
       }
       for (int sfb = s0; sfb < 12; sfb++) {
         const int nb = sfb < 6 ? slen1 : slen2;
-        for (int win = 0; win < 3; win++) sfs[3 * sfb + win] = (uint8_t)(nb ? r.bits(nb) : 0u);
+        for (int win = 0; win < 3; win++) sf.put_s(3 * sfb + win, nb ? r.bits(nb) : 0u);
       }
       break;
     }
@@ -316,11 +333,11 @@ MP3G_HD_INLINE void decode_job(const mp3g_hjob& job, uint64_t j, const uint64_t*
       for (int part = 0; part < 4; part++) {
         const int nb = J.slen[part];
         for (int n = 0; n < (int)J.nsf[part]; n++, k++) {
-          const uint8_t v = (uint8_t)(nb ? r.bits(nb) : 0u);
+          const uint32_t v = nb ? r.bits(nb) : 0u;
           if (lng) {
-            if (k < 22) sfl[k] = v;
+            if (k < 22) sf.put_l(k, v);
           } else if (k < 39) {
-            sfs[k] = v;
+            sf.put_s(k, v);
           }
         }
       }
@@ -355,19 +372,21 @@ MP3G_HD_INLINE void decode_job(const mp3g_hjob& job, uint64_t j, const uint64_t*
     count1 = i;
     if (r.pos > pend + 1) count1 = i >= 4 ? i - 4 : 0;  // the last word overran its part
   }
-  out.finish(i);
+  const int z = out.finish(i);
   for (int k = count1; k < i; k++) row[k] = 0;  // lines the overrun check removed
   C.count1 = (uint16_t)count1;
+  return z;
 }
 
 // decode_job straight from the main data in memory (stream byte order; must
 // be 8-byte aligned and readable up to 8 bytes past the last bit_end).
-MP3G_HD_INLINE void decode_job_direct(const mp3g_hjob& job, uint64_t j, const uint8_t* md, mp3g_granule* gran,
+MP3G_HD_INLINE int decode_job_direct(const mp3g_hjob& job, uint64_t j, const uint8_t* md, mp3g_granule* gran,
                                       int16_t* coef, const uint16_t* T, const uint32_t* s_root,
                                       const uint32_t* s_lin) {
   const uint64_t base = job_base(job);
   const uint32_t nw = job.bit_end > base ? (uint32_t)((job.bit_end - base + 63) >> 6) : 0u;
-  decode_job<true>(job, j, reinterpret_cast<const uint64_t*>(md + (base >> 3)), nw, gran, coef, T, s_root, s_lin);
+  return decode_job<true>(job, j, reinterpret_cast<const uint64_t*>(md + (base >> 3)), nw, gran, coef, T, s_root,
+                          s_lin);
 }
 
 }  // namespace huff

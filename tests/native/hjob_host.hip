@@ -12,7 +12,8 @@ extern "C" int hjob_decode_host(const mp3g_hjob* jobs, uint64_t n_granules, cons
   static const bool ok = mp3g::build_huff_lut(&lut);
   if (!ok) return 1;
   for (uint64_t j = 0; j < 2 * n_granules; j++)
-    mp3g::huff::decode_job_direct(jobs[j], j, md, gran, coef, lut.e, lut.root, lut.linbits);
+    mp3g::huff::zero_fill_row(coef + j * MP3G_LINES,
+                              mp3g::huff::decode_job_direct(jobs[j], j, md, gran, coef, lut.e, lut.root, lut.linbits));
   return 0;
 }
 
@@ -46,12 +47,14 @@ extern "C" int hjob_decode_host_staged(const mp3g_hjob* jobs, uint64_t n_granule
       }
     for (uint64_t j = j0; j < j1; j++) {
       if (!staged) {
-        mp3g::huff::decode_job_direct(jobs[j], j, md, gran, coef, lut.e, lut.root, lut.linbits);
+        mp3g::huff::zero_fill_row(coef + j * MP3G_LINES, mp3g::huff::decode_job_direct(jobs[j], j, md, gran, coef,
+                                                                                      lut.e, lut.root, lut.linbits));
         continue;
       }
       const uint32_t off = jobs[j].sf_kind != MP3G_SF_NONE ? (uint32_t)((mp3g::huff::job_base(jobs[j]) - lo) >> 6) : 0;
-      mp3g::huff::decode_job<false>(jobs[j], j, stage.data() + off, (uint32_t)nwords - off, gran, coef, lut.e,
-                                    lut.root, lut.linbits);
+      const int z = mp3g::huff::decode_job<false>(jobs[j], j, stage.data() + off, (uint32_t)nwords - off, gran, coef,
+                                                  lut.e, lut.root, lut.linbits);
+      mp3g::huff::zero_fill_row(coef + j * MP3G_LINES, z);
     }
   }
   return 0;

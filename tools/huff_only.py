@@ -26,6 +26,15 @@ def main():
     s = mp3g.scan_streams(datas, n_threads=16)
     n = len(s["granules"])
     print(f"granules {n} main data {s['main_data'].nbytes} B, prep {time.perf_counter() - t:.1f} s", flush=True)
+    sort_g = int(os.environ.get("HUFF_SORT", "0"))
+    if sort_g:  # timing experiment only: jobs reordered by big_values within groups (outputs land permuted)
+        jobs = s["jobs"].copy()
+        m = len(jobs) // sort_g * sort_g
+        key = jobs["big_values"][:m].reshape(-1, sort_g)
+        o = np.argsort(key, axis=1, kind="stable") + (np.arange(m // sort_g) * sort_g)[:, None]
+        jobs[:m] = jobs[:m][o.reshape(-1)]
+        s = dict(s, jobs=jobs)
+        print(f"jobs sorted by big_values within groups of {sort_g}")
     dev = torch.device("cuda:0")
     d_g = torch.from_numpy(s["granules"].view(np.uint8).copy()).to(dev)
     d_j = torch.from_numpy(s["jobs"].view(np.uint8).copy()).to(dev)
