@@ -15,6 +15,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
 #include <cstdint>
 
 #include "../../include/mp3g.h"
@@ -231,19 +232,43 @@ MP3G_HD_INLINE void zero_fill_row(int16_t* row, int z) {
   for (int k = z; k < MP3G_LINES; k += 8) *reinterpret_cast<uint4*>(row + k) = make_uint4(0u, 0u, 0u, 0u);
 }
 
-// Scale-factor destination: scalefac_l[22] / scalefac_s[13][3] of the channel.
-struct SfSink {
-  uint8_t* l;
-  uint8_t* s;
-  MP3G_HD_INLINE void put_l(int k, uint32_t v) { l[k] = (uint8_t)v; }
-  MP3G_HD_INLINE void put_s(int k, uint32_t v) { s[k] = (uint8_t)v; }
+// MPEG-1 scale factors of a channel, collected in registers: bytes [8, 72)
+// of the mp3g_channel (scalefac_l from byte 11, scalefac_s from byte 33) as
+// 16 dwords, written with 6 vector stores instead of up to 61 scattered byte
+// stores.  Every factor is put at most once, into a zeroed byte, and the
+// indices are compile-time constants once the loops are unrolled.
+struct SfRegs {
+  uint32_t r[16] = {};
+  MP3G_HD_INLINE void put_l(int k, uint32_t v) { r[(3 + k) >> 2] |= v << (8 * ((3 + k) & 3)); }
+  MP3G_HD_INLINE void put_s(int k, uint32_t v) { r[(25 + k) >> 2] |= v << (8 * ((25 + k) & 3)); }
+  // channel bytes [11, 72) (bytes 8..10, subblock_gain, belong to the scan);
+  // ch selects the alignment of the channel inside its 160-byte granule
+  MP3G_HD_INLINE void store(mp3g_channel& C, int ch) const {
+    uint8_t* cb = reinterpret_cast<uint8_t*>(&C);
+    cb[11] = (uint8_t)(r[0] >> 24);
+    *reinterpret_cast<uint32_t*>(cb + 12) = r[1];
+    if (ch == 0) {  // cb = granule + 8
+      *reinterpret_cast<uint2*>(cb + 16) = make_uint2(r[2], r[3]);
+      *reinterpret_cast<uint4*>(cb + 24) = make_uint4(r[4], r[5], r[6], r[7]);
+      *reinterpret_cast<uint4*>(cb + 40) = make_uint4(r[8], r[9], r[10], r[11]);
+      *reinterpret_cast<uint4*>(cb + 56) = make_uint4(r[12], r[13], r[14], r[15]);
+    } else {  // cb = granule + 80
+      *reinterpret_cast<uint4*>(cb + 16) = make_uint4(r[2], r[3], r[4], r[5]);
+      *reinterpret_cast<uint4*>(cb + 32) = make_uint4(r[6], r[7], r[8], r[9]);
+      *reinterpret_cast<uint4*>(cb + 48) = make_uint4(r[10], r[11], r[12], r[13]);
+      *reinterpret_cast<uint2*>(cb + 64) = make_uint2(r[14], r[15]);
+    }
+  }
 };
+static_assert(offsetof(mp3g_channel, scalefac_l) == 11 && offsetof(mp3g_channel, scalefac_s) == 33 &&
+                  offsetof(mp3g_granule, ch) == 8 && sizeof(mp3g_channel) == 72,
+              "SfRegs byte layout");
 
 // MPEG-1 long-block scale factors (maindata.go:233-279): parts in `read` are
-// read from the stream, parts in `store` are written to sfl.
+// read from the stream, parts in `store` are kept.
 template <bool kSwap>
 MP3G_HD_INLINE void sf_mpeg1_long(Reader<kSwap>& r, int slen1, int slen2, uint32_t read, uint32_t store,
-                                              SfSink& sf) {
+                                              SfRegs& sf) {
 #pragma unroll
   for (int part = 0; part < 4; part++) {
     if (!((read >> part) & 1u)) continue;
@@ -282,7 +307,7 @@ MP3G_HD_INLINE int decode_job(const mp3g_hjob& job, uint64_t j, const uint64_t* 
     return 0;
   }
   mp3g_channel& C = gran[j >> 1].ch[j & 1];
-  SfSink sf{C.scalefac_l, &C.scalefac_s[0][0]};
+  SfRegs sf;
 
   const uint64_t base = job_base(J);
   Reader<kSwap> r;
@@ -315,12 +340,11 @@ MP3G_HD_INLINE int decode_job(const mp3g_hjob& job, uint64_t j, const uint64_t* 
     case MP3G_SF_MPEG1_SHORT:
     case MP3G_SF_MPEG1_MIXED: {
       r.seek(part2);
-      int s0 = 0;
-      if (J.sf_kind == MP3G_SF_MPEG1_MIXED) {
+      const bool mixed = J.sf_kind == MP3G_SF_MPEG1_MIXED;
+      if (mixed)
         for (int sfb = 0; sfb < 8; sfb++) sf.put_l(sfb, slen1 ? r.bits(slen1) : 0u);
-        s0 = 3;
-      }
-      for (int sfb = s0; sfb < 12; sfb++) {
+      for (int sfb = 0; sfb < 12; sfb++) {  // from band 3 when mixed
+        if (mixed && sfb < 3) continue;
         const int nb = sfb < 6 ? slen1 : slen2;
         for (int win = 0; win < 3; win++) sf.put_s(3 * sfb + win, nb ? r.bits(nb) : 0u);
       }
@@ -334,16 +358,18 @@ MP3G_HD_INLINE int decode_job(const mp3g_hjob& job, uint64_t j, const uint64_t* 
         const int nb = J.slen[part];
         for (int n = 0; n < (int)J.nsf[part]; n++, k++) {
           const uint32_t v = nb ? r.bits(nb) : 0u;
-          if (lng) {
-            if (k < 22) sf.put_l(k, v);
+          if (lng) {  // runtime indices: plain byte stores
+            if (k < 22) C.scalefac_l[k] = (uint8_t)v;
           } else if (k < 39) {
-            sf.put_s(k, v);
+            (&C.scalefac_s[0][0])[k] = (uint8_t)v;
           }
         }
       }
       break;
     }
   }
+
+  if (J.sf_kind <= MP3G_SF_MPEG1_MIXED) sf.store(C, (int)(j & 1));
 
   // ---- Huffman (maindata/huffman.go:27-138) ----
   int i = 0, count1 = 0;
