@@ -8,6 +8,7 @@
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <new>
 #include <thread>
 #include <vector>
@@ -19,10 +20,30 @@
 using namespace mp3g;
 using host::St;
 
+namespace {
+
+// An uninitialised array (the merge overwrites every byte; zeroing hundreds
+// of MB first would cost as much as the copy).
+template <class T>
+struct Buf {
+  std::unique_ptr<T[]> p;
+  size_t n = 0;
+  bool alloc(size_t count) {
+    p.reset(new (std::nothrow) T[std::max<size_t>(count, 1)]);
+    n = p ? count : 0;
+    return (bool)p;
+  }
+  T* data() const { return p.get(); }
+  size_t size() const { return n; }
+  T& operator[](size_t i) const { return p[i]; }
+};
+
+}  // namespace
+
 struct mp3g_scan {
-  std::vector<mp3g_granule> gran;
-  std::vector<mp3g_hjob> jobs;
-  std::vector<uint8_t> md;
+  Buf<mp3g_granule> gran;
+  Buf<mp3g_hjob> jobs;
+  Buf<uint8_t> md;
   std::vector<mp3g_stream> streams;
   std::vector<int> status;
 };
@@ -82,29 +103,38 @@ int mp3g_scan_streams(uint32_t n_streams, const uint8_t* const* datas, const siz
   mp3g_scan* s = new (std::nothrow) mp3g_scan;
   if (!s) return abi_fail(MP3G_ERR_OUT_OF_MEMORY, "scan");
   std::vector<StreamScan> per(n_streams);
-  std::atomic<uint32_t> next{0};
-  auto work = [&]() {
-    for (uint32_t k; (k = next.fetch_add(1)) < n_streams;) scan_all(datas[k], lens[k], &per[k]);
-  };
   const int nt = std::max(1, std::min<int>(n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency(),
                                            (int)std::max<uint32_t>(1, n_streams)));
-  std::vector<std::thread> pool;
-  for (int t = 1; t < nt; t++) pool.emplace_back(work);
-  work();
-  for (auto& t : pool) t.join();
-  uint64_t ng = 0, nmd = 0;
-  for (const StreamScan& p : per) {
-    ng += p.gran.size();
-    nmd += (p.md.size() + 15) & ~(size_t)15;  // each stream's bytes 16-B aligned
+  auto parallel = [&](auto&& fn) {  // fn(k) for every stream, on nt threads
+    std::atomic<uint32_t> next{0};
+    auto work = [&]() {
+      for (uint32_t k; (k = next.fetch_add(1)) < n_streams;) fn(k);
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nt; t++) pool.emplace_back(work);
+    work();
+    for (auto& t : pool) t.join();
+  };
+  parallel([&](uint32_t k) { scan_all(datas[k], lens[k], &per[k]); });
+
+  // where each stream lands; each stream's main data 16-B aligned, 16 zero
+  // bytes of padding after the last (the device reads whole 8-B words)
+  std::vector<uint64_t> g_at(n_streams + 1), m_at(n_streams + 1);
+  for (uint32_t k = 0; k < n_streams; k++) {
+    g_at[k + 1] = g_at[k] + per[k].gran.size();
+    m_at[k + 1] = m_at[k] + ((per[k].md.size() + 15) & ~(size_t)15);
   }
-  s->gran.resize(ng);
-  s->jobs.resize(2 * ng);
-  s->md.assign(nmd + 16, 0);  // + padding for the device's 32-bit window loads
+  const uint64_t ng = g_at[n_streams], nmd = m_at[n_streams];
+  if (!s->gran.alloc(ng) || !s->jobs.alloc(2 * ng) || !s->md.alloc(nmd + 16)) {
+    delete s;
+    return abi_fail(MP3G_ERR_OUT_OF_MEMORY, "scan buffers");
+  }
   s->streams.resize(n_streams);
   s->status.resize(n_streams);
-  uint64_t g = 0, m = 0;
-  for (uint32_t k = 0; k < n_streams; k++) {
-    const StreamScan& p = per[k];
+  std::memset(s->md.data() + nmd, 0, 16);
+  parallel([&](uint32_t k) {
+    StreamScan& p = per[k];
+    const uint64_t g = g_at[k], m = m_at[k];
     s->streams[k].first_granule = g;
     s->streams[k].n_granules = (uint32_t)p.gran.size();
     s->streams[k].flags = 0;
@@ -119,9 +149,11 @@ int mp3g_scan_streams(uint32_t n_streams, const uint8_t* const* datas, const siz
       s->jobs[2 * g + i] = J;
     }
     if (!p.md.empty()) std::memcpy(&s->md[m], p.md.data(), p.md.size());
-    g += p.gran.size();
-    m += (p.md.size() + 15) & ~(size_t)15;
-  }
+    std::memset(&s->md[m + p.md.size()], 0, m_at[k + 1] - m - p.md.size());
+    std::vector<mp3g_granule>().swap(p.gran);  // release as we go
+    std::vector<mp3g_hjob>().swap(p.jobs);
+    std::vector<uint8_t>().swap(p.md);
+  });
   *out = s;
   return MP3G_OK;
 }
