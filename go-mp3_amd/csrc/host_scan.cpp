@@ -78,6 +78,9 @@ void scan_all(const uint8_t* data, size_t len, StreamScan* out) {
     return;
   }
   out->md.reserve(len);
+  const size_t frames_est = len / 96 + 16;  // >= 1 frame per 96 bytes at 8 kbps... an estimate, not a bound
+  out->gran.reserve(2 * frames_est);
+  out->jobs.reserve(4 * frames_est);
   host::FrameScanner sc;
   host::ScannedFrame f;
   for (;;) {
