@@ -228,7 +228,9 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
   }
   __syncthreads();  // the only workgroup barrier: the waves are independent from here on
   const int lane = threadIdx.x & (kLanes - 1);
-  const uint32_t ci = blockIdx.x * kWaves + (threadIdx.x >> 6);
+  // wave-uniform in an SGPR: the chunk descriptor then comes in by scalar
+  // loads and its fields (pointers, counts) stay out of the VGPR budget
+  const uint32_t ci = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + (threadIdx.x >> 6));
   if (ci >= n_chunks) return;
   WaveSmem& s = wsm[threadIdx.x >> 6];
   const ChunkDesc cd = chunks[ci];
@@ -264,6 +266,23 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
 
   if (w < end) load_granule(s, gran, coef, w, lane);
   wave_sync();
+
+  // PCM of a granule is stored during the next granule's front end: a VMEM
+  // store's VGPRs may not be overwritten until it completes (the compiler
+  // puts an s_waitcnt vmcnt(0) before the first reuse), so stores issued at
+  // the end of a granule stalled the wave right after them.  pk[] = one dword
+  // (L, R) per lane and slot pair, pend_g = the granule they belong to.
+  uint32_t pk[9];
+  uint32_t pend_g = ~0u;
+  const int hi = lane >> 5;
+  auto store_pcm = [&]() {
+    if (pend_g != ~0u) {
+      uint32_t* P = reinterpret_cast<uint32_t*>(pcm + (size_t)pend_g * 1152);
+#pragma unroll
+      for (int p = 0; p < 9; p++) P[32 * (2 * p + hi) + k] = pk[p];
+      pend_g = ~0u;
+    }
+  };
 
   if constexpr (kStamp) tprev = __builtin_amdgcn_s_memtime();
   for (uint32_t g = w; g < end; g++) {
@@ -441,6 +460,9 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
         x[17 - i] = self(upper, li * cs - dn[i] * ca, li);
       }
     }
+    // the previous granule's PCM (see pk[]); after the stereo stage, whose
+    // table loads would otherwise wait for these stores (vmcnt is in order)
+    store_pcm();
 
     stamp(2);
     // ---- IMDCT + overlap + frequency inversion ----
@@ -610,22 +632,16 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       // (L, R) sample pairs without LDS staging: one v_permlane32_swap per slot
       // pair hands lane i slot 2p's (L, R) and lane 32 + i slot 2p + 1's, so
       // every lane stores one dword per slot pair and the wave 2 x 128
-      // contiguous bytes.  Mono: both halves of the dword are the channel
-      // (frame.go:671-678).
-      uint32_t* P = reinterpret_cast<uint32_t*>(pcm + (size_t)g * 1152);
-      const int hi = lane >> 5;
+      // contiguous bytes.  Mono: the swap hands lane i channel 0's slot 2p and
+      // lane 32 + i its slot 2p + 1, stored in both halves (frame.go:671-678).
 #pragma unroll
       for (int p = 0; p < 9; p++) {
         const int a = (int)__builtin_amdgcn_fmed3f(acc[2 * p], -32767.0f, 32767.0f);
         const int b = (int)__builtin_amdgcn_fmed3f(acc[2 * p + 1], -32767.0f, 32767.0f);
-        if (nch == 2) {
-          const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
-          P[32 * (2 * p + hi) + k] = ((uint32_t)r[0] & 0xffffu) | ((uint32_t)r[1] << 16);
-        } else if (!hi) {
-          P[32 * (2 * p) + k] = ((uint32_t)a & 0xffffu) | ((uint32_t)a << 16);
-          P[32 * (2 * p + 1) + k] = ((uint32_t)b & 0xffffu) | ((uint32_t)b << 16);
-        }
+        const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+        pk[p] = ((uint32_t)r[0] & 0xffffu) | ((uint32_t)(nch == 2 ? r[1] : r[0]) << 16);
       }
+      pend_g = g;
     }
     wave_sync();  // ring reads done
     stamp(6);
@@ -638,6 +654,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     wave_sync();
     stamp(7);
   }
+  store_pcm();
   if constexpr (kStamp) {
     if (lane == 0)
       for (int p = 0; p < kPhases; p++) stamps[(size_t)ci * kPhases + p] = ph[p];

@@ -144,6 +144,8 @@ const char* mp3g_status_string(int s) {
     case MP3G_ERR_PARSE: return "bitstream parse error";
     case MP3G_EOF: return "end of stream";
     case MP3G_ERR_UNSUPPORTED: return "unsupported stream";
+    case MP3G_ERR_NO_XING_HEADER: return "lameinfo: no Xing/Info header found";
+    case MP3G_ERR_UNEXPECTED_EOF: return "unexpected EOF";
   }
   return "unknown status";
 }

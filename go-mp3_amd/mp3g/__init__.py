@@ -40,7 +40,9 @@ assert STREAM_DTYPE.itemsize == 16 and STATE_DTYPE.itemsize == 12800
 MODE_EXACT, MODE_FAST, FLAG_CHECKED, FLAG_KERNEL_V1, FLAG_HOST_HUFFMAN = 0, 1, 0x100, 0x200, 0x400
 STATE_IN, STATE_OUT = 1, 2
 STATUS = {0: "ok", 1: "invalid argument", 2: "invalid granule", 3: "no device", 4: "device error",
-          5: "out of memory", 6: "parse error", 7: "eof", 8: "unsupported"}
+          5: "out of memory", 6: "parse error", 7: "eof", 8: "unsupported", 9: "no Xing/Info header",
+          10: "unexpected EOF"}
+ERR_NO_XING_HEADER, ERR_UNEXPECTED_EOF, EOF = 9, 10, 7
 
 
 class Mp3gError(RuntimeError):
@@ -87,6 +89,10 @@ def lib():
         L.mp3g_scan_streams.argtypes = [u32, vp, vp, C.c_int, C.POINTER(vp)]
         L.mp3g_scan_buffers.argtypes = [vp, C.POINTER(u64), C.POINTER(u64)] + [C.POINTER(vp)] * 5
         L.mp3g_scan_free.argtypes = [vp]
+        L.mp3g_lame_parse.argtypes = [vp, C.c_size_t, C.POINTER(_LameInfo)]
+        L.mp3g_lame_parse_reader.argtypes = [vp, C.c_size_t, C.POINTER(_LameInfo), C.POINTER(C.c_size_t)]
+        L.mp3g_lame_total_delay.argtypes = [C.POINTER(_LameInfo)]
+        L.mp3g_lame_total_padding.argtypes = [C.POINTER(_LameInfo)]
         L.mp3g_huffman_execute.argtypes = [C.c_int, vp, u64, vp, vp, vp, vp]
         L.mp3g_decode_streams.argtypes = [C.c_int, u32, vp, vp, C.c_int, u32, C.POINTER(vp), C.POINTER(u64),
                                           vp, vp]
@@ -244,6 +250,81 @@ def huffman_execute(d_jobs, n_granules, d_main_data, d_granules, d_coeffs, strea
         return C.c_void_p(x.data_ptr() if hasattr(x, "data_ptr") else int(x))
     _check(lib().mp3g_huffman_execute(device, p(d_jobs), n_granules, p(d_main_data), p(d_granules),
                                       p(d_coeffs), C.c_void_p(stream) if stream else None))
+
+
+class _LameInfo(C.Structure):
+    """mp3g_lame_info (include/mp3g.h)."""
+    _fields_ = [("is_xing", C.c_uint32), ("flags", C.c_uint32), ("frame_count", C.c_uint32),
+                ("byte_count", C.c_uint32), ("toc", C.c_uint8 * 100), ("vbr_scale", C.c_uint32),
+                ("has_lame", C.c_uint32), ("lame_version", C.c_uint8 * 12), ("encoder_delay", C.c_uint16),
+                ("encoder_padding", C.c_uint16)]
+
+
+assert C.sizeof(_LameInfo) == 140
+
+FLAG_FRAME_COUNT, FLAG_BYTE_COUNT, FLAG_TOC, FLAG_VBR_SCALE = 0x1, 0x2, 0x4, 0x8
+DECODER_DELAY = 529
+
+
+class LameInfo:
+    """lameinfo.Info (lameinfo/lameinfo.go:20-111), parsed by libmp3g (row f4)."""
+
+    def __init__(self, raw):
+        self._raw = raw
+        self.is_xing = bool(raw.is_xing)
+        self.flags = raw.flags
+        self.frame_count = raw.frame_count
+        self.byte_count = raw.byte_count
+        self.toc = bytes(raw.toc)
+        self.vbr_scale = raw.vbr_scale
+        # the 9 stored bytes, NULs included, as Go's string(frame[pos:pos+9])
+        self.lame_version = bytes(raw.lame_version[:9]).decode("latin-1") if raw.has_lame else ""
+        self.encoder_delay = raw.encoder_delay
+        self.encoder_padding = raw.encoder_padding
+
+    def has_frame_count(self):
+        return bool(self.flags & FLAG_FRAME_COUNT)
+
+    def has_byte_count(self):
+        return bool(self.flags & FLAG_BYTE_COUNT)
+
+    def has_toc(self):
+        return bool(self.flags & FLAG_TOC)
+
+    def has_vbr_scale(self):
+        return bool(self.flags & FLAG_VBR_SCALE)
+
+    def has_lame_info(self):
+        return self.lame_version != ""
+
+    def total_delay(self):
+        return lib().mp3g_lame_total_delay(C.byref(self._raw))
+
+    def total_padding(self):
+        return lib().mp3g_lame_total_padding(C.byref(self._raw))
+
+
+def lame_parse(frame):
+    """lameinfo.Parse: raises Mp3gError(ERR_NO_XING_HEADER) like ErrNoXingHeader."""
+    raw = _LameInfo()
+    b = bytes(frame)
+    st = lib().mp3g_lame_parse(b, len(b), C.byref(raw))
+    if st:
+        raise Mp3gError(st, STATUS.get(st, ""))
+    return LameInfo(raw)
+
+
+def lame_parse_reader(data):
+    """lameinfo.ParseFromReader on a reader over `data`: (LameInfo, bytes read);
+    io.EOF / io.ErrUnexpectedEOF / ErrNoXingHeader raise Mp3gError(EOF /
+    ERR_UNEXPECTED_EOF / ERR_NO_XING_HEADER)."""
+    raw = _LameInfo()
+    b = bytes(data)
+    used = C.c_size_t()
+    st = lib().mp3g_lame_parse_reader(b, len(b), C.byref(raw), C.byref(used))
+    if st:
+        raise Mp3gError(st, STATUS.get(st, ""))
+    return LameInfo(raw), used.value
 
 
 def decode_streams(datas, mode=MODE_EXACT, n_threads=0, device=0):

@@ -42,7 +42,9 @@ typedef enum mp3g_status {
   MP3G_ERR_OUT_OF_MEMORY = 5,
   MP3G_ERR_PARSE = 6,            /* host bitstream parse error (decoder API) */
   MP3G_EOF = 7,                  /* end of stream (decoder API, io.EOF)      */
-  MP3G_ERR_UNSUPPORTED = 8       /* MPEG 2.5, layer I/II, free format, ...   */
+  MP3G_ERR_UNSUPPORTED = 8,      /* MPEG 2.5, layer I/II, free format, ...   */
+  MP3G_ERR_NO_XING_HEADER = 9,   /* lameinfo.ErrNoXingHeader                 */
+  MP3G_ERR_UNEXPECTED_EOF = 10   /* io.ErrUnexpectedEOF (lameinfo.ParseFromReader) */
 } mp3g_status;
 
 /* ---- boundary input: one granule descriptor ---------------------------- */
@@ -299,6 +301,41 @@ int mp3g_decoder_skip_ns(mp3g_decoder* dec, int64_t delta_ns);
  * written as by mp3g_plan_execute.  Synchronous. */
 int mp3g_plan_debug_phases(mp3g_plan* plan, const mp3g_granule* d_granules, const int16_t* d_coeffs,
                            int16_t* d_pcm, uint64_t* out_cycles, void* hip_stream);
+
+/* ---- Xing / Info / LAME tag (lameinfo/lameinfo.go) ----
+ * The reference's lameinfo package: the tag in the first frame (encoder delay
+ * and padding for gapless playback, frame / byte counts, the VBR seek TOC).
+ * The decoder never reads it (decode.go decodes the tag frame as silence);
+ * callers trim with the two totals.  140 bytes. */
+#define MP3G_XING_FRAME_COUNT 0x0001u /* lameinfo.FlagFrameCount */
+#define MP3G_XING_BYTE_COUNT 0x0002u  /* FlagByteCount */
+#define MP3G_XING_TOC 0x0004u         /* FlagTOC */
+#define MP3G_XING_VBR_SCALE 0x0008u   /* FlagVBRScale */
+#define MP3G_LAME_DECODER_DELAY 529   /* lameinfo.DecoderDelay */
+typedef struct mp3g_lame_info {
+  uint32_t is_xing;         /* Info.IsXing: tag "Xing" (VBR) vs "Info" (CBR) */
+  uint32_t flags;           /* Info.Flags */
+  uint32_t frame_count;     /* Info.FrameCount */
+  uint32_t byte_count;      /* Info.ByteCount */
+  uint8_t toc[100];         /* Info.TOC */
+  uint32_t vbr_scale;       /* Info.VBRScale */
+  uint32_t has_lame;        /* Info.HasLAMEInfo(): LAMEVersion != "" */
+  char lame_version[12];    /* Info.LAMEVersion: the 9 bytes as stored (may hold NULs), zero padded */
+  uint16_t encoder_delay;   /* Info.EncoderDelay */
+  uint16_t encoder_padding; /* Info.EncoderPadding */
+} mp3g_lame_info;
+
+/* lameinfo.Parse (lameinfo.go:139-270): one whole frame incl. its header.
+ * MP3G_OK or MP3G_ERR_NO_XING_HEADER. */
+int mp3g_lame_parse(const uint8_t* frame, size_t len, mp3g_lame_info* out);
+/* lameinfo.ParseFromReader (lameinfo.go:288-328) on a reader positioned at
+ * `data`: reads the header, sizes the frame, reads the frame, parses it.
+ * MP3G_OK, MP3G_ERR_NO_XING_HEADER, MP3G_EOF (io.EOF) or
+ * MP3G_ERR_UNEXPECTED_EOF; *consumed (may be NULL) = bytes read. */
+int mp3g_lame_parse_reader(const uint8_t* data, size_t len, mp3g_lame_info* out, size_t* consumed);
+/* Info.TotalDelay / Info.TotalPadding (lameinfo.go:92-111) */
+int mp3g_lame_total_delay(const mp3g_lame_info* info);
+int mp3g_lame_total_padding(const mp3g_lame_info* info);
 
 #ifdef __cplusplus
 }
