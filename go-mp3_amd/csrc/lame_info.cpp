@@ -148,4 +148,33 @@ int mp3g_lame_total_padding(const mp3g_lame_info* info) {
   return p < 0 ? 0 : p;
 }
 
+// Gapless trim of a decoded stream (the use the reference documents for the
+// two totals, lameinfo.go:86-111; it never applies them itself): go-mp3
+// decodes the tag frame as silence (decode.go), so the caller passes the
+// samples that frame produced (1152 MPEG-1, 576 MPEG-2) and gets the range of
+// the n_samples to keep.
+int mp3g_lame_trim(const mp3g_lame_info* info, uint64_t n_samples, uint32_t tag_frame_samples, uint64_t* first,
+                   uint64_t* count) {
+  if (!info || !first || !count) return mp3g::abi_fail(MP3G_ERR_INVALID_ARGUMENT, "null argument");
+  const uint64_t skip = (uint64_t)tag_frame_samples + (uint64_t)mp3g_lame_total_delay(info);
+  const uint64_t drop = (uint64_t)mp3g_lame_total_padding(info);
+  *first = skip < n_samples ? skip : n_samples;
+  *count = n_samples > skip + drop ? n_samples - skip - drop : 0;
+  return MP3G_OK;
+}
+
+// Xing TOC seek: the byte offset of `percent` (0..100) of the playback time,
+// TOC[i] / 256 of the byte count, interpolated between entries (the table
+// Info.TOC holds, lameinfo.go:33-35).  Without a TOC or byte count, linear.
+uint64_t mp3g_lame_toc_offset(const mp3g_lame_info* info, double percent) {
+  if (!info) return 0;
+  const double p = percent < 0.0 ? 0.0 : percent > 100.0 ? 100.0 : percent;
+  const double bytes = (double)info->byte_count;
+  if (!(info->flags & MP3G_XING_TOC) || !(info->flags & MP3G_XING_BYTE_COUNT)) return (uint64_t)(p / 100.0 * bytes);
+  int i = (int)p;
+  if (i > 99) i = 99;
+  const double a = info->toc[i], b = i < 99 ? info->toc[i + 1] : 256.0;
+  return (uint64_t)((a + (b - a) * (p - i)) / 256.0 * bytes);
+}
+
 }  // extern "C"

@@ -336,6 +336,14 @@ int mp3g_lame_parse_reader(const uint8_t* data, size_t len, mp3g_lame_info* out,
 /* Info.TotalDelay / Info.TotalPadding (lameinfo.go:92-111) */
 int mp3g_lame_total_delay(const mp3g_lame_info* info);
 int mp3g_lame_total_padding(const mp3g_lame_info* info);
+/* Gapless trim of n_samples decoded samples (per channel) of a stream whose
+ * first frame held the tag: keep [*first, *first + *count); tag_frame_samples
+ * = what the decoder produced for the tag frame (1152 MPEG-1, 576 MPEG-2).
+ * The reference only exposes the two totals; this applies them. */
+int mp3g_lame_trim(const mp3g_lame_info* info, uint64_t n_samples, uint32_t tag_frame_samples, uint64_t* first,
+                   uint64_t* count);
+/* Xing TOC seek: byte offset of `percent` (0..100) of the playback time. */
+uint64_t mp3g_lame_toc_offset(const mp3g_lame_info* info, double percent);
 
 #ifdef __cplusplus
 }

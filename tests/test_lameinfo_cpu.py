@@ -199,3 +199,21 @@ def test_against_oracle_mutations():
             assert (got_r if isinstance(got_r, str) else _as_oracle(got_r)) == want_r, f.hex()[:80]
             n += 1
     assert n == len(seeds) * 60
+
+
+def test_gapless_trim_and_toc():
+    """The two totals applied to a decoded length (mp3g_lame_trim) and the TOC seek."""
+    data = open(os.path.join(GOLDEN, "classic_lame.mp3"), "rb").read()
+    i, _ = mp3g.lame_parse_reader(data)
+    n = i.frame_count * 1152
+    first, count = i.trim(n)
+    assert first == 1152 + 576 + mp3g.DECODER_DELAY
+    assert count == n - first - (i.encoder_padding - mp3g.DECODER_DELAY)
+    assert i.trim(100) == (100, 0)  # shorter than the delay: nothing kept
+    plain = mp3g.lame_parse(build_test_frame(True, FC, 10))
+    assert plain.trim(10 * 1152, 1152) == (1152 + 529, 10 * 1152 - 1152 - 529)
+    # TOC: monotone in the percentage, 0 at 0 %, within the byte count
+    offs = [i.toc_offset(p) for p in range(0, 101, 5)]
+    assert offs[0] == i.toc[0] * i.byte_count // 256 and offs == sorted(offs) and offs[-1] <= i.byte_count
+    t = mp3g.lame_parse(build_test_frame(True, BC | TOC, byte_count=25600))
+    assert t.toc_offset(10) == 10 * 100 and t.toc_offset(10.5) == 1050
