@@ -27,6 +27,7 @@
 // windows) -> 11 resident waves per CU.
 // (compiled as part of kernels.hip, after granule_common.hip)
 #pragma clang fp contract(fast)
+#include "dct4_18.h"
 #include "xlane.h"
 
 namespace mp3g {
@@ -62,7 +63,6 @@ constexpr int kRing = kHist + 18;
 // read-only tables, one copy per workgroup
 struct __align__(16) SharedSmem {
   float win[4][36];    // imdctWinData
-  f2 c36p[9][18];      // distinct cosN36 columns as pairs (col q, col 18+q): [q][m]
   float c12t[12][8];   // cosN12 transposed [p][m] (rows padded to 2 x float4)
   float isr[8][2];
   float dct[32][16];   // FastTables::dct rows (one row per lane, read once per granule)
@@ -211,10 +211,6 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
   {
     const int t = threadIdx.x;
     for (int e = t; e < 4 * 36; e += kLanes * kWaves) (&sh.win[0][0])[e] = (&g_fast.win[0][0])[e];
-    for (int e = t; e < 9 * 18; e += kLanes * kWaves) {
-      const int q = e / 18, m = e % 18;
-      sh.c36p[q][m] = (f2){g_fast.c36[m][q], g_fast.c36[m][9 + q]};
-    }
     for (int e = t; e < 12 * 8; e += kLanes * kWaves) {
       const int p = e >> 3, m = e & 7;
       sh.c12t[p][m] = m < 6 ? g_fast.cos12[m][p] : 0.0f;
@@ -492,17 +488,17 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
         }
       } else {
         const float* W = sh.win[bt];
+        // the 18 distinct sums are a DCT-IV of size 18 (dct4_18.h):
+        // sum_m x[m] cosN36[m][q] = X[9+q], sum_m x[m] cosN36[m][18+q] = -X[8-q]
+        float X[18];
+        dct4::dct4_18(x, X);
 #pragma unroll
         for (int q = 0; q < 9; q++) {
-          // (sum_m x[m] cosN36[m][q], sum_m x[m] cosN36[m][18+q]) as one packed chain
-          f2 z = bcast(0.0f);
-          const f2* c = sh.c36p[q];
-#pragma unroll
-          for (int m = 0; m < 18; m++) z = pfma(bcast(x[m]), c[m], z);
-          o[q] = z.x * W[q] + st[q];
-          o[17 - q] = -z.x * W[17 - q] + st[17 - q];
-          st[q] = self(act, z.y * W[18 + q], st[q]);
-          st[17 - q] = self(act, z.y * W[35 - q], st[17 - q]);
+          const float za = X[9 + q], zb = -X[8 - q];
+          o[q] = za * W[q] + st[q];
+          o[17 - q] = -za * W[17 - q] + st[17 - q];
+          st[q] = self(act, zb * W[18 + q], st[q]);
+          st[17 - q] = self(act, zb * W[35 - q], st[17 - q]);
         }
       }
 #pragma unroll
@@ -565,14 +561,21 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       wave_sync();
       if (need_v && act) {
         const f2* E = &s.a.eo[ch][0][(k & 1) * 16];
+        // X_k of the slot pairs (6*third + 2pp, +1), pp = 0..2: six independent
+        // packed chains (three slot pairs x even / odd q) instead of three
+        // serial 16-FMA chains
+        f2 acc[3][2];
+#pragma unroll
+        for (int pp = 0; pp < 3; pp++) acc[pp][0] = acc[pp][1] = bcast(0.0f);
+#pragma unroll
+        for (int q = 0; q < 16; q++)
+#pragma unroll
+          for (int pp = 0; pp < 3; pp++) acc[pp][q & 1] = pfma(bcast(dct[q]), E[32 * pp + q], acc[pp][q & 1]);
 #pragma unroll
         for (int pp = 0; pp < 3; pp++) {
-          // X_k of the slot pair (6*third + 2pp, +1)
-          f2 acc = bcast(0.0f);
-#pragma unroll
-          for (int q = 0; q < 16; q++) acc = pfma(bcast(dct[q]), E[32 * pp + q], acc);
-          s.ring[ch][kHist + 6 * third + 2 * pp][k] = acc.x;
-          s.ring[ch][kHist + 6 * third + 2 * pp + 1][k] = acc.y;
+          const f2 a = acc[pp][0] + acc[pp][1];
+          s.ring[ch][kHist + 6 * third + 2 * pp][k] = a.x;
+          s.ring[ch][kHist + 6 * third + 2 * pp + 1][k] = a.y;
         }
       }
       wave_sync();
