@@ -1,4 +1,4 @@
-// dct4_18.h -- 18-point DCT-IV for the fast kernel's long-block IMDCT
+// dct4_18.h -- IMDCT constants of the fast kernel: the 18-point DCT-IV for long blocks
 // (granule_fast.hip).  The reference's IMDCT-36 (imdct.go:21-108) sums
 // x[m] cosN36[m][p] over m = 0..17 directly; its 18 distinct outputs are a
 // DCT-IV of size 18,
@@ -81,6 +81,24 @@ __host__ __device__ __forceinline__ void dct4_18(const float x[18], float X[18])
     X[17 - 2 * k] = __builtin_fmaf(yr, s, -yi * c);
   }
 }
+
+// Short blocks (imdct.go:88-94): the 12-point IMDCT of each window as a
+// direct sum with literal coefficients (6 inputs; no table in LDS either).
+// cosN12[m][p] of imdct.go as [p][m] (dsp_tables.cpp build_tables values)
+constexpr float kCos12[12][6] = {{6.087614298e-01f, -9.238795042e-01f, -1.305261850e-01f, 9.914448857e-01f, -3.826834261e-01f, -7.933533192e-01f},
+                                   {3.826834261e-01f, -9.238795042e-01f, 9.238795042e-01f, -3.826834261e-01f, -3.826834261e-01f, 9.238795042e-01f},
+                                   {1.305261850e-01f, -3.826834261e-01f, 6.087614298e-01f, -7.933533192e-01f, 9.238795042e-01f, -9.914448857e-01f},
+                                   {-1.305261850e-01f, 3.826834261e-01f, -6.087614298e-01f, 7.933533192e-01f, -9.238795042e-01f, 9.914448857e-01f},
+                                   {-3.826834261e-01f, 9.238795042e-01f, -9.238795042e-01f, 3.826834261e-01f, 3.826834261e-01f, -9.238795042e-01f},
+                                   {-6.087614298e-01f, 9.238795042e-01f, 1.305261850e-01f, -9.914448857e-01f, 3.826834261e-01f, 7.933533192e-01f},
+                                   {-7.933533192e-01f, 3.826834261e-01f, 9.914448857e-01f, 1.305261850e-01f, -9.238795042e-01f, -6.087614298e-01f},
+                                   {-9.238795042e-01f, -3.826834261e-01f, 3.826834261e-01f, 9.238795042e-01f, 9.238795042e-01f, 3.826834261e-01f},
+                                   {-9.914448857e-01f, -9.238795042e-01f, -7.933533192e-01f, -6.087614298e-01f, -3.826834261e-01f, -1.305261850e-01f},
+                                   {-9.914448857e-01f, -9.238795042e-01f, -7.933533192e-01f, -6.087614298e-01f, -3.826834261e-01f, -1.305261850e-01f},
+                                   {-9.238795042e-01f, -3.826834261e-01f, 3.826834261e-01f, 9.238795042e-01f, 9.238795042e-01f, 3.826834261e-01f},
+                                   {-7.933533192e-01f, 3.826834261e-01f, 9.914448857e-01f, 1.305261850e-01f, -9.238795042e-01f, -6.087614298e-01f}};
+// the short-block window (imdct.go block type 2)
+constexpr float kWin12[12] = {1.305261850e-01f, 3.826834261e-01f, 6.087614298e-01f, 7.933533192e-01f, 9.238795042e-01f, 9.914448857e-01f, 9.914448857e-01f, 9.238795042e-01f, 7.933533192e-01f, 6.087614298e-01f, 3.826834261e-01f, 1.305261850e-01f};
 
 }  // namespace dct4
 }  // namespace mp3g

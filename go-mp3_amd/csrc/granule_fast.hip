@@ -63,7 +63,6 @@ constexpr int kRing = kHist + 18;
 // read-only tables, one copy per workgroup
 struct __align__(16) SharedSmem {
   float win[4][36];    // imdctWinData
-  float c12t[12][8];   // cosN12 transposed [p][m] (rows padded to 2 x float4)
   float isr[8][2];
   float dct[32][16];   // FastTables::dct rows (one row per lane, read once per granule)
   float dwin[32][16];  // FastTables::dwin rows, pre-scaled by 32767
@@ -211,10 +210,6 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
   {
     const int t = threadIdx.x;
     for (int e = t; e < 4 * 36; e += kLanes * kWaves) (&sh.win[0][0])[e] = (&g_fast.win[0][0])[e];
-    for (int e = t; e < 12 * 8; e += kLanes * kWaves) {
-      const int p = e >> 3, m = e & 7;
-      sh.c12t[p][m] = m < 6 ? g_fast.cos12[m][p] : 0.0f;
-    }
     for (int e = t; e < 16; e += kLanes * kWaves) (&sh.isr[0][0])[e] = (&g_fast.is_ratio[0][0])[e];
     for (int e = t; e < 32 * 16; e += kLanes * kWaves) {
       (&sh.dct[0][0])[e] = (&g_fast.dct[0][0])[e];
@@ -480,8 +475,8 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
             if (p < 0 || p >= 12) continue;
             float sum = 0.0f;
 #pragma unroll
-            for (int m = 0; m < 6; m++) sum += x[wi + 3 * m] * sh.c12t[p][m];
-            raw += sum * sh.win[2][p];
+            for (int m = 0; m < 6; m++) sum += x[wi + 3 * m] * dct4::kCos12[p][m];
+            raw += sum * dct4::kWin12[p];
           }
           if (pos < 18) o[pos] = raw + st[pos];
           else st[pos - 18] = self(act, raw, st[pos - 18]);

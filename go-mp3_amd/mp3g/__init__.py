@@ -9,6 +9,7 @@ Boundary structs mirror include/mp3g.h exactly (asserted sizes below).
 """
 import ctypes as C
 import os
+import time
 
 import numpy as np
 
@@ -230,7 +231,9 @@ def scan_streams(datas, n_threads=0):
     (two per granule), main_data (uint8, padded), streams, end_status."""
     bufs, ptrs, lens = _stream_args(datas)
     h = C.c_void_p()
+    t0 = time.perf_counter()
     _check(lib().mp3g_scan_streams(len(datas), ptrs, lens, n_threads, C.byref(h)))
+    scan_s = time.perf_counter() - t0
     try:
         ng, nmd = C.c_uint64(), C.c_uint64()
         pg, pj, pm, ps, pst = (C.c_void_p() for _ in range(5))
@@ -241,7 +244,7 @@ def scan_streams(datas, n_threads=0):
                 "jobs": _copy_out(pj, 2 * n * HJOB_DTYPE.itemsize, HJOB_DTYPE),
                 "main_data": _copy_out(pm, nmd.value, np.uint8),
                 "streams": _copy_out(ps, len(datas) * STREAM_DTYPE.itemsize, STREAM_DTYPE),
-                "end_status": _copy_out(pst, len(datas) * 4, np.int32)}
+                "end_status": _copy_out(pst, len(datas) * 4, np.int32), "scan_s": scan_s}
     finally:
         lib().mp3g_scan_free(h)
 
