@@ -64,7 +64,7 @@ constexpr int kRing = kHist + 18;
 struct __align__(16) SharedSmem {
   float win[4][36];    // imdctWinData
   float isr[8][2];
-  float dct[32][16];   // FastTables::dct rows (one row per lane, read once per granule)
+  float dctp[32][16];  // matrixing coefficients per lane k, in DPP rotation order (see the matrixing)
   float dwin[32][16];  // FastTables::dwin rows, pre-scaled by 32767
   // FastTables::lband: read per lane every granule, so it lives in LDS -- a
   // vector global load there would wait (vmcnt is in order) for the previous
@@ -77,7 +77,6 @@ struct __align__(16) SharedSmem {
 struct __align__(16) WaveSmem {
   union {
     int16_t raw[2][576];  // Huffman integers of the current granule
-    f2 eo[2][3][32];      // folded matrixing input of 6 slots [ch][slot pair][k]: even k<16, odd 16+k
   } a;
   float ring[2][kRing][32];
   // requantization exponents n4 of the long bands [ch][sfb] and short bands [ch][sfb][win]
@@ -212,7 +211,12 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     for (int e = t; e < 4 * 36; e += kLanes * kWaves) (&sh.win[0][0])[e] = (&g_fast.win[0][0])[e];
     for (int e = t; e < 16; e += kLanes * kWaves) (&sh.isr[0][0])[e] = (&g_fast.is_ratio[0][0])[e];
     for (int e = t; e < 32 * 16; e += kLanes * kWaves) {
-      (&sh.dct[0][0])[e] = (&g_fast.dct[0][0])[e];
+      // lane k = 16 * row + r computes X_m, m = 2r + row; at rotation n it holds
+      // the folded value of lane (r - n) & 15 of its row (DPP row_ror:n), i.e.
+      // E_even[(r - n) & 15] in row 0 and E_odd[15 - ((r - n) & 15)] in row 1
+      const int kk = e >> 4, n = e & 15, r = kk & 15, row = kk >> 4;
+      const int src = (r - n) & 15, q = row ? 15 - src : src;
+      sh.dctp[kk][n] = g_fast.dct[2 * r + row][q];
       (&sh.dwin[0][0])[e] = (&g_fast.dwin[0][0])[e] * 32767.0f;
     }
     for (int e = t; e < kCombos * 32; e += kLanes * kWaves) (&sh.lband[0][0])[e] = (&g_fast.lband[0][0])[e];
@@ -530,52 +534,54 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       }
     }
 
-    // ---- matrixing, in two halves of 9 time slots: even/odd fold of S across
-    //      the subband pair (k, 31-k), then X_k of each slot (lane = (ch, m = k)) ----
-    float dct[16];
+    // ---- matrixing: even/odd fold of S across the subband pair (k, 31-k), then
+    //      X_m = sum_q dct[m][q] E_par(m)[q] for every slot.  After the fold, row 0
+    //      of a channel's 32 lanes holds E_even[q] in lane q and row 1 holds
+    //      E_odd[q] in lane 31-q, so lane (row, r) computes m = 2r + row from its
+    //      own row only: 16 DPP row rotations feed the FMAs directly (no LDS
+    //      round trip of the folded values: the kernel is LDS-bound) ----
+    float dcp[16];
     {
-      const float4* d4 = reinterpret_cast<const float4*>(&sh.dct[k][0]);
+      const float4* d4 = reinterpret_cast<const float4*>(&sh.dctp[k][0]);
 #pragma unroll
       for (int q = 0; q < 4; q++) {
         const float4 v = d4[q];
-        dct[4 * q] = v.x;
-        dct[4 * q + 1] = v.y;
-        dct[4 * q + 2] = v.z;
-        dct[4 * q + 3] = v.w;
+        dcp[4 * q] = v.x;
+        dcp[4 * q + 1] = v.y;
+        dcp[4 * q + 2] = v.z;
+        dcp[4 * q + 3] = v.w;
       }
     }
+    const int mo = 2 * (k & 15) + (k >> 4);
 #pragma unroll
     for (int third = 0; third < 3; third++) {
+      float ex[3], ey[3];
 #pragma unroll
       for (int pp = 0; pp < 3; pp++) {
         const int j = 6 * third + 2 * pp;
-        const f2 v = {o[j], o[j + 1]};
-        const f2 oth = {xl::xor31(o[j]), xl::xor31(o[j + 1])};
-        if (act) s.a.eo[ch][pp][k < 16 ? k : 47 - k] = k < 16 ? v + oth : oth - v;
+        const float ox = xl::xor31(o[j]), oy = xl::xor31(o[j + 1]);
+        ex[pp] = k < 16 ? o[j] + ox : ox - o[j];
+        ey[pp] = k < 16 ? o[j + 1] + oy : oy - o[j + 1];
       }
-      wave_sync();
       if (need_v && act) {
-        const f2* E = &s.a.eo[ch][0][(k & 1) * 16];
-        // X_k of the slot pairs (6*third + 2pp, +1), pp = 0..2: six independent
-        // packed chains (three slot pairs x even / odd q) instead of three
-        // serial 16-FMA chains
-        f2 acc[3][2];
+        float ax[3][2], ay[3][2];
 #pragma unroll
-        for (int pp = 0; pp < 3; pp++) acc[pp][0] = acc[pp][1] = bcast(0.0f);
-#pragma unroll
-        for (int q = 0; q < 16; q++)
-#pragma unroll
-          for (int pp = 0; pp < 3; pp++) acc[pp][q & 1] = pfma(bcast(dct[q]), E[32 * pp + q], acc[pp][q & 1]);
+        for (int pp = 0; pp < 3; pp++) ax[pp][0] = ax[pp][1] = ay[pp][0] = ay[pp][1] = 0.0f;
 #pragma unroll
         for (int pp = 0; pp < 3; pp++) {
-          const f2 a = acc[pp][0] + acc[pp][1];
-          s.ring[ch][kHist + 6 * third + 2 * pp][k] = a.x;
-          s.ring[ch][kHist + 6 * third + 2 * pp + 1][k] = a.y;
+          ax[pp][0] = ex[pp] * dcp[0];
+          ay[pp][0] = ey[pp] * dcp[0];
+          xl::rot_fma15(ax[pp][0], ax[pp][1], ay[pp][0], ay[pp][1], ex[pp], ey[pp], dcp);
+        }
+#pragma unroll
+        for (int pp = 0; pp < 3; pp++) {
+          s.ring[ch][kHist + 6 * third + 2 * pp][mo] = ax[pp][0] + ax[pp][1];
+          s.ring[ch][kHist + 6 * third + 2 * pp + 1][mo] = ay[pp][0] + ay[pp][1];
         }
       }
-      wave_sync();
       if (third) stamp(3 + third);
     }
+    wave_sync();  // ring slots of this granule written before the window reads them
 
     // ---- next granule in: raw/eo (dead after the matrixing) and the
     //      descriptor (not read again this granule) take the prefetch now,
