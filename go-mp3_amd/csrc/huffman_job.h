@@ -381,13 +381,34 @@ MP3G_HD_INLINE int decode_job(const mp3g_hjob& job, uint64_t j, const uint64_t* 
     const uint32_t root0 = s_root[J.table_select[0]], root1 = s_root[J.table_select[1]],
                    root2 = s_root[J.table_select[2]], qroot = s_root[32 + J.count1_table];
     const uint32_t lb0 = s_lin[J.table_select[0]], lb1 = s_lin[J.table_select[1]], lb2 = s_lin[J.table_select[2]];
-    for (; i < bv2; i += 2) {
-      const uint32_t root = i < r1 ? root0 : i < r2 ? root1 : root2;
-      const uint32_t lb = i < r1 ? lb0 : i < r2 ? lb1 : lb2;
-      int a, b, c, d;
-      decode_sym(r, T, root, lb, a, b, c, d);
-      out.put(i, a, b);
+    // big values four pairs (one 16-B block) per step: the block's words sit
+    // in fixed registers (no per-pair slot select) and full blocks are stored
+    // straight away; the block holding bv2 (when it is not a multiple of 8)
+    // goes on in the writer for the count1 quads
+    for (int i0 = 0; i0 < bv2; i0 += 8) {
+      uint32_t w[4];
+#pragma unroll
+      for (int sl = 0; sl < 4; sl++) {
+        const int ii = i0 + 2 * sl;
+        w[sl] = 0u;
+        if (ii < bv2) {
+          const uint32_t root = ii < r1 ? root0 : ii < r2 ? root1 : root2;
+          const uint32_t lb = ii < r1 ? lb0 : ii < r2 ? lb1 : lb2;
+          int a, b, c, d;
+          decode_sym(r, T, root, lb, a, b, c, d);
+          w[sl] = (uint32_t)(uint16_t)(int16_t)a | ((uint32_t)(uint16_t)(int16_t)b << 16);
+        }
+      }
+      if (i0 + 8 <= bv2) {
+        *reinterpret_cast<uint4*>(row + i0) = make_uint4(w[0], w[1], w[2], w[3]);
+      } else {
+        out.b0 = w[0];
+        out.b1 = w[1];
+        out.b2 = w[2];
+        out.b3 = w[3];
+      }
     }
+    i = bv2;
     while (i <= 572 && r.pos <= pend) {
       int a, b, c, d;
       decode_sym(r, T, qroot, 0u, a, b, c, d);
