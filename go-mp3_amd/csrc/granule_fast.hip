@@ -59,6 +59,13 @@ __device__ __forceinline__ int kPretab(int sfb) { return (int)((0x2fe95400000ull
 // suffice (the 16th V block of Frame.vVec is never read again).
 constexpr int kHist = 15;
 constexpr int kRing = kHist + 18;
+// window passes per granule: each X pair feeds up to 8 outputs; one pass of 18
+// outputs reads every pair once (64 LDS reads), two passes of 9 re-read the
+// 14 shared pairs (92) but hold half the accumulators
+#ifndef MP3G_WIN_PASSES
+#define MP3G_WIN_PASSES 1
+#endif
+constexpr int kWinPasses = MP3G_WIN_PASSES;
 
 // read-only tables, one copy per workgroup
 struct __align__(16) SharedSmem {
@@ -616,22 +623,23 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       // 9 outputs keep the live pairs + accumulators within the register budget.
       float acc[18];
       const float* R = &s.ring[ch][0][0];
+      constexpr int kOut = 18 / kWinPasses;  // outputs per pass
 #pragma unroll
-      for (int pass = 0; pass < 2; pass++) {
-        f2 acc2[9];
+      for (int pass = 0; pass < kWinPasses; pass++) {
+        f2 acc2[kOut];
 #pragma unroll
-        for (int i = 0; i < 9; i++) acc2[i] = bcast(0.0f);
+        for (int i = 0; i < kOut; i++) acc2[i] = bcast(0.0f);
 #pragma unroll
-        for (int u = 9 * pass - 14; u < 9 * pass + 9; u++) {
+        for (int u = kOut * pass - 14; u < kOut * pass + kOut; u++) {
           const f2 P = {R[(kHist + u) * 32 + ia], R[(kHist + u - 1) * 32 + ib]};
 #pragma unroll
           for (int t = 0; t < 8; t++) {
-            const int i = u + 2 * t - 9 * pass;
-            if (i >= 0 && i < 9) acc2[i] = pfma((f2){dw[2 * t], dw[2 * t + 1]}, P, acc2[i]);
+            const int i = u + 2 * t - kOut * pass;
+            if (i >= 0 && i < kOut) acc2[i] = pfma((f2){dw[2 * t], dw[2 * t + 1]}, P, acc2[i]);
           }
         }
 #pragma unroll
-        for (int i = 0; i < 9; i++) acc[9 * pass + i] = acc2[i].x + acc2[i].y;
+        for (int i = 0; i < kOut; i++) acc[kOut * pass + i] = acc2[i].x + acc2[i].y;
       }
       // (L, R) sample pairs without LDS staging: one v_permlane32_swap per slot
       // pair hands lane i slot 2p's (L, R) and lane 32 + i slot 2p + 1's, so
