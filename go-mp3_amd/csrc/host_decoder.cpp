@@ -96,8 +96,13 @@ struct mp3g_decoder {
   std::vector<mp3g_hjob> h_jobs;
   std::vector<int16_t> h_pcm;
   std::vector<uint32_t> frame_pcm_bytes;  // PCM bytes of each frame of the last batch
+  std::vector<int64_t> frame_src;         // source position after each frame of the last batch
   std::vector<size_t> frame_ends;         // end offset in buf of each buffered frame
-  size_t next_end = 0;                    // index into frame_ends of the current frame
+  std::vector<int64_t> frame_src_ends;    // source position after each buffered frame
+  // index into frame_ends of the frame the reference read last: Decoder.Read
+  // reads one frame once its d.buf is empty (decode.go:70-80), so this is the
+  // frame being served, advanced lazily at the next Read like the reference
+  size_t next_end = 0;
 
   ~mp3g_decoder() {
     int prev = -1;
@@ -135,6 +140,7 @@ struct mp3g_decoder {
     h_coef.clear();
     h_jobs.clear();
     frame_pcm_bytes.clear();
+    frame_src.clear();
     St st = St::kOk;
     if (gpu_huffman()) {
       // drop main data no later frame can reach (the reservoir is < 2 KB)
@@ -153,6 +159,7 @@ struct mp3g_decoder {
           h_jobs.push_back(f.job[gr][1]);
         }
         frame_pcm_bytes.push_back((uint32_t)(f.n_granules * MP3G_PCM_BYTES_PER_GRANULE));
+        frame_src.push_back(src.pos);
       }
     } else {
       host::ParsedFrame f;
@@ -164,6 +171,7 @@ struct mp3g_decoder {
           h_coef.insert(h_coef.end(), f.coef[gr], f.coef[gr] + MP3G_COEF_PER_GRANULE);
         }
         frame_pcm_bytes.push_back((uint32_t)(f.n_granules * MP3G_PCM_BYTES_PER_GRANULE));
+        frame_src.push_back(src.pos);
       }
     }
     const int err = st == St::kOk ? MP3G_OK : to_status(st);
@@ -247,6 +255,7 @@ struct mp3g_decoder {
     buf.insert(buf.end(), p, p + n * MP3G_PCM_BYTES_PER_GRANULE);
     size_t end = buf.size() - n * MP3G_PCM_BYTES_PER_GRANULE;
     for (uint32_t b : frame_pcm_bytes) frame_ends.push_back(end += b);
+    frame_src_ends.insert(frame_src_ends.end(), frame_src.begin(), frame_src.end());
     return MP3G_OK;
   }
 
@@ -254,7 +263,16 @@ struct mp3g_decoder {
     buf.clear();
     buf_off = 0;
     frame_ends.clear();
+    frame_src_ends.clear();
     next_end = 0;
+  }
+
+  // Where the reference's source stands: right after the last frame it read.
+  // The read-ahead has parsed further; a seek that reads nothing (to or past
+  // the end, decode.go:110-113) must leave the source there, so that the next
+  // Read decodes the frame the reference decodes.
+  void rewind_read_ahead() {
+    if (next_end < frame_src_ends.size()) src.seek(frame_src_ends[next_end], 0, nullptr);
   }
 
   // readFrame for Read: decode the next batch (read-ahead grows to 1024 frames)
@@ -262,6 +280,7 @@ struct mp3g_decoder {
     if (pending != MP3G_OK) {
       const int e = pending;
       pending = MP3G_OK;
+      frame_src_ends.clear();  // the reference's source now stands after the failed frame
       return e;
     }
     buf_reset();
@@ -438,6 +457,7 @@ int mp3g_decoder_seek(mp3g_decoder* d, int64_t offset, int whence, int64_t* newp
     default: return abi_fail(MP3G_ERR_INVALID_ARGUMENT, "mp3: invalid whence");
   }
   d->pos = npos;
+  d->rewind_read_ahead();
   d->buf_reset();
   d->reset_reservoir();  // d.frame = nil
   d->md.clear();
@@ -471,6 +491,7 @@ int mp3g_decoder_seek(mp3g_decoder* d, int64_t offset, int whence, int64_t* newp
   const int64_t off = need == 2 ? d->bytes_per_frame + d->pos % d->bytes_per_frame : d->pos;
   if (off > (int64_t)ref_len) return abi_fail(MP3G_ERR_UNSUPPORTED, "slice out of range (the reference panics)");
   d->buf_off = (size_t)off;
+  d->next_end = (size_t)need - 1;  // the reference read `need` frames, the last is being served
   *newpos = npos;
   return MP3G_OK;
 }

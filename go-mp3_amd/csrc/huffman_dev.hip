@@ -79,7 +79,11 @@ huffman_kernel(const mp3g_hjob* __restrict__ jobs, uint64_t n_jobs, const uint8_
   int z = MP3G_LINES;  // first line this lane's row still needs zeroed
   if (valid) {
     if (staged) {
-      const uint32_t off = reads ? (uint32_t)((base - lo) >> 6) : 0u;
+      // a corrupt stream's part 2 can start past the wave's span (part2_3_length
+      // sums overrunning the main data): clamp, so the reader's nw never wraps
+      // and its loads stay inside this wave's staging buffer
+      const uint64_t off64 = reads ? (base - lo) >> 6 : 0ull;
+      const uint32_t off = (uint32_t)(off64 < nwords ? off64 : nwords);
       z = decode_job<false>(J, j, &stage[wv][off], (uint32_t)nwords - off, gran, coef, T, s_root, s_lin);
     } else {
       z = decode_job_direct(J, j, md, gran, coef, T, s_root, s_lin);

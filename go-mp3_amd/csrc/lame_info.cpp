@@ -165,16 +165,26 @@ int mp3g_lame_trim(const mp3g_lame_info* info, uint64_t n_samples, uint32_t tag_
 
 // Xing TOC seek: the byte offset of `percent` (0..100) of the playback time,
 // TOC[i] / 256 of the byte count, interpolated between entries (the table
-// Info.TOC holds, lameinfo.go:33-35).  Without a TOC or byte count, linear.
-uint64_t mp3g_lame_toc_offset(const mp3g_lame_info* info, double percent) {
-  if (!info) return 0;
+// Info.TOC holds, lameinfo.go:33-35).  The byte count is the tag's own
+// (flag 0x2) or, when the tag has none, `stream_bytes` from the caller; without
+// a TOC the offset is linear in that count.  *offset = 0 and
+// MP3G_ERR_INVALID_ARGUMENT when neither count is known (stream_bytes = 0).
+int mp3g_lame_toc_offset(const mp3g_lame_info* info, double percent, uint64_t stream_bytes, uint64_t* offset) {
+  if (!info || !offset) return mp3g::abi_fail(MP3G_ERR_INVALID_ARGUMENT, "null argument");
+  *offset = 0;
+  const bool own = info->flags & MP3G_XING_BYTE_COUNT;
+  if (!own && stream_bytes == 0) return mp3g::abi_fail(MP3G_ERR_INVALID_ARGUMENT, "no byte count in the tag or from the caller");
   const double p = percent < 0.0 ? 0.0 : percent > 100.0 ? 100.0 : percent;
-  const double bytes = (double)info->byte_count;
-  if (!(info->flags & MP3G_XING_TOC) || !(info->flags & MP3G_XING_BYTE_COUNT)) return (uint64_t)(p / 100.0 * bytes);
+  const double bytes = own ? (double)info->byte_count : (double)stream_bytes;
+  if (!(info->flags & MP3G_XING_TOC)) {
+    *offset = (uint64_t)(p / 100.0 * bytes);
+    return MP3G_OK;
+  }
   int i = (int)p;
   if (i > 99) i = 99;
   const double a = info->toc[i], b = i < 99 ? info->toc[i + 1] : 256.0;
-  return (uint64_t)((a + (b - a) * (p - i)) / 256.0 * bytes);
+  *offset = (uint64_t)((a + (b - a) * (p - i)) / 256.0 * bytes);
+  return MP3G_OK;
 }
 
 }  // extern "C"

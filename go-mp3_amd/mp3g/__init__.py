@@ -95,8 +95,8 @@ def lib():
         L.mp3g_lame_total_delay.argtypes = [C.POINTER(_LameInfo)]
         L.mp3g_lame_total_padding.argtypes = [C.POINTER(_LameInfo)]
         L.mp3g_lame_trim.argtypes = [C.POINTER(_LameInfo), u64, u32, C.POINTER(u64), C.POINTER(u64)]
-        L.mp3g_lame_toc_offset.argtypes = [C.POINTER(_LameInfo), C.c_double]
-        L.mp3g_lame_toc_offset.restype = u64
+        L.mp3g_lame_toc_offset.argtypes = [C.POINTER(_LameInfo), C.c_double, u64, C.POINTER(u64)]
+        L.mp3g_lame_toc_offset.restype = C.c_int
         L.mp3g_huffman_execute.argtypes = [C.c_int, vp, u64, vp, vp, vp, vp]
         L.mp3g_decode_streams.argtypes = [C.c_int, u32, vp, vp, C.c_int, u32, C.POINTER(vp), C.POINTER(u64),
                                           vp, vp]
@@ -315,9 +315,12 @@ class LameInfo:
         _check(lib().mp3g_lame_trim(C.byref(self._raw), n_samples, tag_frame_samples, C.byref(a), C.byref(b)))
         return a.value, b.value
 
-    def toc_offset(self, percent):
-        """Byte offset of `percent` of the playback time from the Xing TOC."""
-        return lib().mp3g_lame_toc_offset(C.byref(self._raw), float(percent))
+    def toc_offset(self, percent, stream_bytes=0):
+        """Byte offset of `percent` of the playback time from the Xing TOC; the
+        tag's byte count, else `stream_bytes` (Mp3gError when neither is known)."""
+        out = C.c_uint64()
+        _check(lib().mp3g_lame_toc_offset(C.byref(self._raw), float(percent), int(stream_bytes), C.byref(out)))
+        return out.value
 
 
 def lame_parse(frame):

@@ -342,8 +342,12 @@ int mp3g_lame_total_padding(const mp3g_lame_info* info);
  * The reference only exposes the two totals; this applies them. */
 int mp3g_lame_trim(const mp3g_lame_info* info, uint64_t n_samples, uint32_t tag_frame_samples, uint64_t* first,
                    uint64_t* count);
-/* Xing TOC seek: byte offset of `percent` (0..100) of the playback time. */
-uint64_t mp3g_lame_toc_offset(const mp3g_lame_info* info, double percent);
+/* Xing TOC seek: *offset = byte offset of `percent` (0..100) of the playback
+ * time, from Info.TOC (lameinfo.go:33-35) scaled by the tag's byte count
+ * (flag 0x2) or, when the tag carries none, by `stream_bytes` (the caller's
+ * audio byte length); linear without a TOC.  MP3G_ERR_INVALID_ARGUMENT (and
+ * *offset = 0) when neither byte count is known. */
+int mp3g_lame_toc_offset(const mp3g_lame_info* info, double percent, uint64_t stream_bytes, uint64_t* offset);
 
 #ifdef __cplusplus
 }

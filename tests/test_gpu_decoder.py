@@ -91,6 +91,33 @@ def test_random_seek_read_sequence(gpu, sample_files, mode):
             assert d.pos == o.pos and d.position_ns == o.position_ns, (name, step)
 
 
+@pytest.mark.parametrize("mode", [0, 0x400])
+@pytest.mark.parametrize("name", ["classic_lame.mp3", "mpeg2.mp3"])
+@pytest.mark.parametrize("consumed", [0, 1, 4608, 3 * 4608 + 17, 200_000])
+def test_seek_past_end_then_read(gpu, sample_files, mode, name, consumed):
+    """A seek to or past Length() reads no frame (decode.go:110-113): the next
+    Read continues with the frame after the last one the reference read, from
+    zero state and an empty reservoir -- not from where the read-ahead stopped."""
+    d, o = both(gpu, sample_files[name], mode=mode)
+    while consumed > 0:
+        st, b = d.read(consumed)
+        st2, b2 = o.read(consumed)
+        assert st == ST[st2] and b == b2
+        consumed -= len(b)
+    for off, whence in ((0, 2), (12345, 2), (o.length + 4, 0)):
+        r, r2 = d.seek(off, whence), o.seek(off, whence)
+        assert (r[0], r[1]) == (ST[r2[0]], r2[1])
+        got = want = b""
+        for _ in range(5):  # more than one frame, each Read returns at most one
+            st, b = d.read(10000)
+            st2, b2 = o.read(10000)
+            assert st == ST[st2]
+            got += b
+            want += b2
+        assert len(got) > 4608 and got == want
+        assert d.pos == o.pos
+
+
 def test_time_api_values(gpu, sample_files):
     d, o = both(gpu, sample_files["mpeg2.mp3"])
     assert d.seek_to_time_ns(30_000_000_000) == 0 and o.seek_to_time_ns(30_000_000_000) == 0

@@ -217,3 +217,11 @@ def test_gapless_trim_and_toc():
     assert offs[0] == i.toc[0] * i.byte_count // 256 and offs == sorted(offs) and offs[-1] <= i.byte_count
     t = mp3g.lame_parse(build_test_frame(True, BC | TOC, byte_count=25600))
     assert t.toc_offset(10) == 10 * 100 and t.toc_offset(10.5) == 1050
+    assert t.toc_offset(10, stream_bytes=999) == 10 * 100  # the tag's own count wins
+    # no byte count in the tag: the caller's stream length, or an error (not a silent 0)
+    nb = mp3g.lame_parse(build_test_frame(True, TOC))
+    with pytest.raises(mp3g.Mp3gError):
+        nb.toc_offset(50)
+    assert nb.toc_offset(0, stream_bytes=25600) == nb.toc[0] * 100
+    lin = mp3g.lame_parse(build_test_frame(True, FC, 10))
+    assert lin.toc_offset(25, stream_bytes=4000) == 1000
