@@ -203,7 +203,8 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
                     const int16_t* __restrict__ coef, const mp3g_state* __restrict__ state_in,
                     mp3g_state* __restrict__ state_out, int16_t* __restrict__ pcm,
                     unsigned long long* __restrict__ stamps) {
-  unsigned long long ph[kPhases] = {}, tprev = 0;
+  unsigned long long ph[kPhases] = {}, tprev = 0, rt[4] = {};
+  if constexpr (kStamp) rt[0] = __builtin_amdgcn_s_memrealtime();
   auto stamp = [&](int p) {
     if constexpr (kStamp) {
       const unsigned long long t = __builtin_amdgcn_s_memtime();
@@ -286,8 +287,25 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     }
   };
 
-  if constexpr (kStamp) tprev = __builtin_amdgcn_s_memtime();
+  if constexpr (kStamp) {
+    tprev = __builtin_amdgcn_s_memtime();
+    rt[1] = __builtin_amdgcn_s_memrealtime();
+  }
+  // Progress-balanced issue priority.  The SIMD arbitrates VALU issue by
+  // priority, then age (MI355X_MICROARCH.md, two waves per SIMD), so at equal
+  // priority the oldest of the ~3 waves sharing a SIMD runs ahead and the
+  // youngest finishes last, alone and latency-bound (c2 timeline: loop spans
+  // 34 .. 101 us for identical chunks).  A wave with more of its chunk left
+  // takes a higher priority, which keeps the co-resident waves abreast.
+  const uint32_t span = end - w;
   for (uint32_t g = w; g < end; g++) {
+    {
+      const uint32_t q = (4u * (end - g) - 1u) / span;  // 3 (most left) .. 0
+      if (q >= 3) __builtin_amdgcn_s_setprio(3);
+      else if (q == 2) __builtin_amdgcn_s_setprio(2);
+      else if (q == 1) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+    }
     const bool out = g >= out_first;
     // does a replayed granule's V feed anything? (see v2 / DESIGN.md halo)
     bool need_v = true;
@@ -667,10 +685,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     stamp(7);
   }
   store_pcm();
-  if constexpr (kStamp) {
-    if (lane == 0)
-      for (int p = 0; p < kPhases; p++) stamps[(size_t)ci * kPhases + p] = ph[p];
-  }
+  if constexpr (kStamp) rt[2] = __builtin_amdgcn_s_memrealtime();
 
   if (cd.flags & kChunkStateOut) {
     mp3g_state* so = state_out + cd.stream;
@@ -679,6 +694,13 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     for (int e = lane; e < 2 * 1024; e += kLanes) {
       const int c = e >> 10, blk = (e >> 6) & 15, i = e & 63;
       so->vvec[c][64 * blk + i] = blk < kHist ? v_from_x(s.ring[c][kHist - 1 - blk], i) : 0.0f;
+    }
+  }
+  if constexpr (kStamp) {
+    rt[3] = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0) {
+      for (int p = 0; p < kPhases; p++) stamps[(size_t)ci * kFastStampSlots + p] = ph[p];
+      for (int p = 0; p < 4; p++) stamps[(size_t)ci * kFastStampSlots + kPhases + p] = rt[p];
     }
   }
 }

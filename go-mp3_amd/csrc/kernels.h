@@ -48,6 +48,9 @@ hipError_t launch_huffman(const mp3g_hjob* d_jobs, uint64_t n_jobs, const uint8_
 
 // Diagnostic: fast kernel with per-phase s_memtime sums (8 per chunk) in d_stamps.
 constexpr int kFastPhases = 8;
+// per chunk: kFastPhases cycle sums, then s_memrealtime (100 MHz) at kernel
+// entry, loop start, loop end and exit
+constexpr int kFastStampSlots = kFastPhases + 4;
 hipError_t launch_fast_stamped(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_granule* d_gran,
                                const int16_t* d_coef, const mp3g_state* d_state_in, mp3g_state* d_state_out,
                                int16_t* d_pcm, unsigned long long* d_stamps, hipStream_t stream);

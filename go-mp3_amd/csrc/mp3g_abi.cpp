@@ -323,28 +323,49 @@ int mp3g_huffman_execute(int device, const mp3g_hjob* d_jobs, uint64_t n_granule
   return MP3G_OK;
 }
 
-int mp3g_plan_debug_phases(mp3g_plan* p, const mp3g_granule* d_gran, const int16_t* d_coef, int16_t* d_pcm,
-                           uint64_t* out_cycles, void* hip_stream) {
-  if (!p || !out_cycles) return fail(MP3G_ERR_INVALID_ARGUMENT, "null argument");
+// stamped launch of a fast plan: kFastStampSlots per chunk into h
+static int run_stamped(mp3g_plan* p, const mp3g_granule* d_gran, const int16_t* d_coef, int16_t* d_pcm,
+                       std::vector<unsigned long long>* h, void* hip_stream) {
   if ((p->mode & 0xffu) != MP3G_MODE_FAST) return fail(MP3G_ERR_INVALID_ARGUMENT, "not a fast-mode plan");
-  for (int i = 0; i < kFastPhases; i++) out_cycles[i] = 0;
-  if (p->chunks.empty()) return MP3G_OK;
   for (const ChunkDesc& c : p->chunks)
     if (c.flags & (kChunkStateIn | kChunkStateOut)) return fail(MP3G_ERR_INVALID_ARGUMENT, "stateful plan");
+  h->assign(p->chunks.size() * kFastStampSlots, 0ull);
+  if (p->chunks.empty()) return MP3G_OK;
   DeviceGuard guard(p->device);
   if (guard.err != hipSuccess) return fail(MP3G_ERR_NO_DEVICE, "hipSetDevice", guard.err);
-  const size_t n = p->chunks.size() * kFastPhases;
   unsigned long long* d_st = nullptr;
-  hipError_t e = hipMalloc(&d_st, n * sizeof(unsigned long long));
+  hipError_t e = hipMalloc(&d_st, h->size() * sizeof(unsigned long long));
   if (e != hipSuccess) return fail(MP3G_ERR_OUT_OF_MEMORY, "hipMalloc(stamps)", e);
   hipStream_t st = static_cast<hipStream_t>(hip_stream);
   e = launch_fast_stamped(p->d_chunks, (uint32_t)p->chunks.size(), d_gran, d_coef, nullptr, nullptr, d_pcm, d_st, st);
-  std::vector<unsigned long long> h(n);
-  if (e == hipSuccess) e = hipMemcpyAsync(h.data(), d_st, n * sizeof(unsigned long long), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(h->data(), d_st, h->size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   (void)hipFree(d_st);
   if (e != hipSuccess) return fail(MP3G_ERR_DEVICE, "stamped launch", e);
-  for (size_t i = 0; i < n; i++) out_cycles[i % kFastPhases] += h[i];
+  return MP3G_OK;
+}
+
+int mp3g_plan_debug_phases(mp3g_plan* p, const mp3g_granule* d_gran, const int16_t* d_coef, int16_t* d_pcm,
+                           uint64_t* out_cycles, void* hip_stream) {
+  if (!p || !out_cycles) return fail(MP3G_ERR_INVALID_ARGUMENT, "null argument");
+  for (int i = 0; i < kFastPhases; i++) out_cycles[i] = 0;
+  std::vector<unsigned long long> h;
+  const int rc = run_stamped(p, d_gran, d_coef, d_pcm, &h, hip_stream);
+  if (rc) return rc;
+  for (size_t i = 0; i < h.size(); i++)
+    if (i % kFastStampSlots < (size_t)kFastPhases) out_cycles[i % kFastStampSlots] += h[i];
+  return MP3G_OK;
+}
+
+int mp3g_plan_debug_timeline(mp3g_plan* p, const mp3g_granule* d_gran, const int16_t* d_coef, int16_t* d_pcm,
+                             uint64_t* out_ticks, void* hip_stream) {
+  if (!p || !out_ticks) return fail(MP3G_ERR_INVALID_ARGUMENT, "null argument");
+  std::vector<unsigned long long> h;
+  const int rc = run_stamped(p, d_gran, d_coef, d_pcm, &h, hip_stream);
+  if (rc) return rc;
+  for (size_t c = 0; c < p->chunks.size(); c++)
+    for (int k = 0; k < 4; k++) out_ticks[4 * c + k] = h[c * kFastStampSlots + kFastPhases + k];
   return MP3G_OK;
 }
 

@@ -81,6 +81,7 @@ def lib():
         L.mp3g_plan_execute.argtypes = [vp, vp, vp, vp, vp, vp, vp]
         L.mp3g_decode_host.argtypes = [C.c_int, vp, vp, u64, vp, u32, vp, vp, vp, u32]
         L.mp3g_plan_debug_phases.argtypes = [vp, vp, vp, vp, C.POINTER(u64), vp]
+        L.mp3g_plan_debug_timeline.argtypes = [vp, vp, vp, vp, C.POINTER(u64), vp]
         i64, sz = C.c_int64, C.c_size_t
         L.mp3g_parse_stream.argtypes = [vp, sz, C.POINTER(vp), C.POINTER(vp), C.POINTER(u64),
                                         C.POINTER(C.c_int)]
@@ -461,6 +462,16 @@ class Plan:
         _check(lib().mp3g_plan_debug_phases(self._h, p(d_gran), p(d_coef), p(d_pcm), out,
                                             C.c_void_p(stream) if stream else None))
         return dict(zip(self.PHASES, list(out)))
+
+    def debug_timeline(self, d_gran, d_coef, d_pcm, stream=None):
+        """Diagnostic (fast plans): [chunks, 4] s_memrealtime ticks (100 MHz) of
+        each wave at entry, loop start, loop end, exit."""
+        n = self.info()["chunks"]
+        out = (C.c_uint64 * max(1, 4 * n))()
+        p = lambda x: C.c_void_p(x.data_ptr() if hasattr(x, "data_ptr") else int(x))
+        _check(lib().mp3g_plan_debug_timeline(self._h, p(d_gran), p(d_coef), p(d_pcm), out,
+                                              C.c_void_p(stream) if stream else None))
+        return np.frombuffer(out, dtype=np.uint64)[:4 * n].reshape(n, 4).copy()
 
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:

@@ -301,6 +301,11 @@ int mp3g_decoder_skip_ns(mp3g_decoder* dec, int64_t delta_ns);
  * written as by mp3g_plan_execute.  Synchronous. */
 int mp3g_plan_debug_phases(mp3g_plan* plan, const mp3g_granule* d_granules, const int16_t* d_coeffs,
                            int16_t* d_pcm, uint64_t* out_cycles, void* hip_stream);
+/* The same instrumented launch; per chunk (out_ticks[4 * chunk + 0..3]) the
+ * wave's s_memrealtime (100 MHz) at kernel entry, at the start and the end of
+ * its granule loop and at exit: the launch's ramp, per-wave span and tail. */
+int mp3g_plan_debug_timeline(mp3g_plan* plan, const mp3g_granule* d_granules, const int16_t* d_coeffs,
+                             int16_t* d_pcm, uint64_t* out_ticks, void* hip_stream);
 
 /* ---- Xing / Info / LAME tag (lameinfo/lameinfo.go) ----
  * The reference's lameinfo package: the tag in the first frame (encoder delay

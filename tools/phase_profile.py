@@ -14,26 +14,37 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 import mp3g  # noqa: E402
 
-cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
-dev = torch.device("cuda:0")
-g, c, streams, info = bench.build_workload(cfg, 0)
-if cfg == "c3":
-    pg, pc, idx = g
-    d_g = torch.from_numpy(pg.view(np.uint8).reshape(len(pg), -1).copy()).to(dev).index_select(
-        0, torch.from_numpy(idx).to(dev)).reshape(-1).contiguous()
-    d_c = torch.from_numpy(pc.reshape(len(pc), -1).copy()).to(dev).index_select(
-        0, torch.from_numpy(idx).to(dev)).reshape(-1).contiguous()
-    n = len(idx)
-else:
-    d_g = torch.from_numpy(g.view(np.uint8).copy()).to(dev)
-    d_c = torch.from_numpy(c.reshape(-1).copy()).to(dev)
-    n = len(g)
-d_pcm = torch.empty(n * 1152, dtype=torch.int16, device=dev)
-plan = mp3g.Plan(streams, mode=mp3g.MODE_FAST)
-plan.execute(d_g, d_c, d_pcm)
-torch.cuda.synchronize()
-ph = plan.debug_phases(d_g, d_c, d_pcm)
-tot = sum(ph.values())
-gran = plan.info()["granules"] + plan.info()["halo_granules"]
-print(json.dumps({"config": cfg, "cycles_per_granule_per_wave": round(tot / gran, 1),
-                  "phases": {k: [round(v / gran, 1), round(v / tot, 4)] for k, v in ph.items()}}, indent=1))
+
+def device_workload(cfg):
+    """bench.py's workload for cfg as device tensors (granules, coefficients, PCM out) + streams."""
+    dev = torch.device("cuda:0")
+    g, c, streams, info = bench.build_workload(cfg, 0)
+    if cfg == "c3":
+        pg, pc, idx = g
+        d_g = torch.from_numpy(pg.view(np.uint8).reshape(len(pg), -1).copy()).to(dev).index_select(
+            0, torch.from_numpy(idx).to(dev)).reshape(-1).contiguous()
+        d_c = torch.from_numpy(pc.reshape(len(pc), -1).copy()).to(dev).index_select(
+            0, torch.from_numpy(idx).to(dev)).reshape(-1).contiguous()
+        n = len(idx)
+    else:
+        d_g = torch.from_numpy(g.view(np.uint8).copy()).to(dev)
+        d_c = torch.from_numpy(c.reshape(-1).copy()).to(dev)
+        n = len(g)
+    return d_g, d_c, torch.empty(n * 1152, dtype=torch.int16, device=dev), streams
+
+
+def main():
+    cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
+    d_g, d_c, d_pcm, streams = device_workload(cfg)
+    plan = mp3g.Plan(streams, mode=mp3g.MODE_FAST)
+    plan.execute(d_g, d_c, d_pcm)
+    torch.cuda.synchronize()
+    ph = plan.debug_phases(d_g, d_c, d_pcm)
+    tot = sum(ph.values())
+    gran = plan.info()["granules"] + plan.info()["halo_granules"]
+    print(json.dumps({"config": cfg, "cycles_per_granule_per_wave": round(tot / gran, 1),
+                      "phases": {k: [round(v / gran, 1), round(v / tot, 4)] for k, v in ph.items()}}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
