@@ -27,6 +27,7 @@
 // windows) -> 11 resident waves per CU.
 // (compiled as part of kernels.hip, after granule_common.hip)
 #pragma clang fp contract(fast)
+#include "dct32.h"
 #include "dct4_18.h"
 #include "xlane.h"
 
@@ -59,6 +60,10 @@ __device__ __forceinline__ int kPretab(int sfb) { return (int)((0x2fe95400000ull
 // suffice (the 16th V block of Frame.vVec is never read again).
 constexpr int kHist = 15;
 constexpr int kRing = kHist + 18;
+// ring row: 32 values + 4 of padding.  144-B rows keep the row-per-lane
+// accesses of the matrixing (16-B reads, 8-B writes by lanes of different
+// rows) free of bank conflicts.
+constexpr int kRow = 36;
 // window passes per granule: each X pair feeds up to 8 outputs; one pass of 18
 // outputs reads every pair once (64 LDS reads), two passes of 9 re-read the
 // 14 shared pairs (92) but hold half the accumulators
@@ -71,7 +76,6 @@ constexpr int kWinPasses = MP3G_WIN_PASSES;
 struct __align__(16) SharedSmem {
   float win[4][36];    // imdctWinData
   float isr[8][2];
-  float dctp[32][16];  // matrixing coefficients per lane k, in DPP rotation order (see the matrixing)
   float dwin[32][16];  // FastTables::dwin rows, pre-scaled by 32767
   // FastTables::lband: read per lane every granule, so it lives in LDS -- a
   // vector global load there would wait (vmcnt is in order) for the previous
@@ -85,7 +89,10 @@ struct __align__(16) WaveSmem {
   union {
     int16_t raw[2][576];  // Huffman integers of the current granule
   } a;
-  float ring[2][kRing][32];
+  // X vectors in dct32::kPosOfM order; the current granule's rows first
+  // receive S (the IMDCT output, one row per slot) and the matrixing turns
+  // them into X in place
+  float ring[2][kRing][kRow];
   // requantization exponents n4 of the long bands [ch][sfb] and short bands [ch][sfb][win]
   int expo[2 * 22 + 2 * 39];
   mp3g_granule desc;
@@ -185,11 +192,12 @@ __device__ __forceinline__ float requant_fast(int xi, int n4) {
 // X of a V block: X[m] = V[m-16] (m >= 16), -V[48-m] (m < 16).
 __device__ __forceinline__ float x_from_v(const float* v, int m) { return m >= 16 ? v[m - 16] : -v[48 - m]; }
 // V of an X vector (inverse identity; V[16] = 0).
+// x holds X in dct32::kPosOfM order.
 __device__ __forceinline__ float v_from_x(const float* x, int i) {
-  if (i < 16) return x[16 + i];
+  if (i < 16) return x[dct32::kPosOfM[16 + i]];
   if (i == 16) return 0.0f;
-  if (i < 48) return -x[48 - i];
-  return -x[i - 48];
+  if (i < 48) return -x[dct32::kPosOfM[48 - i]];
+  return -x[dct32::kPosOfM[i - 48]];
 }
 
 }  // namespace
@@ -218,15 +226,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     const int t = threadIdx.x;
     for (int e = t; e < 4 * 36; e += kLanes * kWaves) (&sh.win[0][0])[e] = (&g_fast.win[0][0])[e];
     for (int e = t; e < 16; e += kLanes * kWaves) (&sh.isr[0][0])[e] = (&g_fast.is_ratio[0][0])[e];
-    for (int e = t; e < 32 * 16; e += kLanes * kWaves) {
-      // lane k = 16 * row + r computes X_m, m = 2r + row; at rotation n it holds
-      // the folded value of lane (r - n) & 15 of its row (DPP row_ror:n), i.e.
-      // E_even[(r - n) & 15] in row 0 and E_odd[15 - ((r - n) & 15)] in row 1
-      const int kk = e >> 4, n = e & 15, r = kk & 15, row = kk >> 4;
-      const int src = (r - n) & 15, q = row ? 15 - src : src;
-      sh.dctp[kk][n] = g_fast.dct[2 * r + row][q];
-      (&sh.dwin[0][0])[e] = (&g_fast.dwin[0][0])[e] * 32767.0f;
-    }
+    for (int e = t; e < 32 * 16; e += kLanes * kWaves) (&sh.dwin[0][0])[e] = (&g_fast.dwin[0][0])[e] * 32767.0f;
     for (int e = t; e < kCombos * 32; e += kLanes * kWaves) (&sh.lband[0][0])[e] = (&g_fast.lband[0][0])[e];
   }
   __syncthreads();  // the only workgroup barrier: the waves are independent from here on
@@ -238,8 +238,9 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
   WaveSmem& s = wsm[threadIdx.x >> 6];
   const ChunkDesc cd = chunks[ci];
   const int ch = lane >> 5, k = lane & 31;
-  const int ia = k < 16 ? 16 + k : (k == 16 ? 0 : 48 - k);
-  const int ib = k < 16 ? 16 - k : k - 16;
+  // ring positions of the two X values the window of output i = k reads
+  const int pa = dct32::kPosOfM[k < 16 ? 16 + k : (k == 16 ? 0 : 48 - k)];
+  const int pb = dct32::kPosOfM[k < 16 ? 16 - k : k - 16];
 
   uint64_t w64;
   int init_in[2];
@@ -263,7 +264,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     for (int e = lane; e < 2 * kHist * 32; e += kLanes) {
       const int c = e / (kHist * 32), blk = (e >> 5) % kHist, m = e & 31;
       const bool in = c ? in1 : in0;
-      s.ring[c][kHist - 1 - blk][m] = in ? x_from_v(&sin->vvec[c][64 * blk], m) : 0.0f;
+      s.ring[c][kHist - 1 - blk][dct32::kPosOfM[m]] = in ? x_from_v(&sin->vvec[c][64 * blk], m) : 0.0f;
     }
   }
 
@@ -318,8 +319,14 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     const mp3g_channel& C = s.desc.ch[act ? ch : 0];
 
 
-    // ---- per-granule front-end parameters: band exponents, band thresholds ----
-    for (int e = lane; e < 2 * 22 + 2 * 39; e += kLanes) {
+    // wave-uniform: every channel of this granule is a long block (no reorder)
+    const bool all_long = __builtin_amdgcn_readfirstlane(
+        !(s.desc.ch[0].win_switch_flag == 1 && s.desc.ch[0].block_type == 2) &&
+        (nch == 1 || !(s.desc.ch[1].win_switch_flag == 1 && s.desc.ch[1].block_type == 2)));
+
+    // ---- per-granule front-end parameters: band exponents (long bands only
+    //      when no channel has short blocks), band thresholds ----
+    for (int e = lane; e < (all_long ? 2 * 22 : 2 * 22 + 2 * 39); e += kLanes) {
       int c, v;
       if (e < 44) {
         c = e >= 22;
@@ -349,10 +356,6 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     // ---- front end: requantize (gather through the reorder), lane = (ch, sb = k) ----
     // the lane's 18 line-info words and raw integers are loaded in bulk first
     float x[18];
-    // wave-uniform: every channel of this granule is a long block (no reorder)
-    const bool all_long = __builtin_amdgcn_readfirstlane(
-        !(s.desc.ch[0].win_switch_flag == 1 && s.desc.ch[0].block_type == 2) &&
-        (nch == 1 || !(s.desc.ch[1].win_switch_flag == 1 && s.desc.ch[1].block_type == 2)));
     if (all_long) {
       int xi[18];
       const uint32_t* rw = reinterpret_cast<const uint32_t*>(&s.a.raw[ch][18 * k]);
@@ -408,7 +411,23 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
 #pragma unroll
       for (int b = 0; b < 14; b++) ns_is += 3 * (int)g_fast.sfb_short[combo][b] < c1r;
       const float inv_sqrt2 = 0.70710678118654752440f;
-      if (!is) {  // MS only (the common joint-stereo case): L' = (l+r)c, R' = (l-r)c
+      if (!is && all_long) {
+        // MS only on long blocks (the common joint-stereo case): lines at or
+        // above max(count1) are 0 in both channels, where (l +- r)c is 0 too,
+        // so every line is transformed.  Two lines per step: one swap gives
+        // lanes < 32 (l, r) of line j and lanes >= 32 those of line j + 1,
+        // (l + r)c, (l - r)c in one packed pair, a second swap hands back
+        // L' / R' of both lines to their channels' lanes.
+#pragma unroll
+        for (int j = 0; j < 18; j += 2) {
+          const auto r = __builtin_amdgcn_permlane32_swap(__float_as_int(x[j]), __float_as_int(x[j + 1]), false, false);
+          const float a = __int_as_float(r[0]), b = __int_as_float(r[1]);
+          const f2 pq = (f2){a + b, a - b} * bcast(inv_sqrt2);
+          const auto r2 = __builtin_amdgcn_permlane32_swap(__float_as_int(pq.x), __float_as_int(pq.y), false, false);
+          x[j] = __int_as_float(r2[0]);
+          x[j + 1] = __int_as_float(r2[1]);
+        }
+      } else if (!is) {  // MS with short blocks: the reorder can move values past count1
         const float sg = ch ? -1.0f : 1.0f;
 #pragma unroll
         for (int j = 0; j < 18; j++) {
@@ -559,53 +578,36 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       }
     }
 
-    // ---- matrixing: even/odd fold of S across the subband pair (k, 31-k), then
-    //      X_m = sum_q dct[m][q] E_par(m)[q] for every slot.  After the fold, row 0
-    //      of a channel's 32 lanes holds E_even[q] in lane q and row 1 holds
-    //      E_odd[q] in lane 31-q, so lane (row, r) computes m = 2r + row from its
-    //      own row only: 16 DPP row rotations feed the FMAs directly (no LDS
-    //      round trip of the folded values: the kernel is LDS-bound) ----
-    float dcp[16];
+    // ---- matrixing (frame.go:642-648): S rows into the ring (lane (ch, sb)
+    //      writes its 18 slots), then one lane per (ch, slot) turns its row into
+    //      the 32 distinct values X of V = synthNWin * S with an in-lane fast
+    //      DCT-II-32 on float pairs (dct32.h), in place ----
+    if (need_v && act) {
+      float* Sc = &s.ring[ch][kHist][k];
+#pragma unroll
+      for (int j = 0; j < 18; j++) Sc[kRow * j] = o[j];
+    }
+    wave_sync();
+    stamp(4);
     {
-      const float4* d4 = reinterpret_cast<const float4*>(&sh.dctp[k][0]);
+      const int slot = lane & 31;  // lane = (ch, slot), slots 0..17
+      if (need_v && act && slot < 18) {
+        float* row = &s.ring[ch][kHist + slot][0];
+        dct32::f2 sp[16], xp[16];
+        const float4* r4 = reinterpret_cast<const float4*>(row);
 #pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const float4 v = d4[q];
-        dcp[4 * q] = v.x;
-        dcp[4 * q + 1] = v.y;
-        dcp[4 * q + 2] = v.z;
-        dcp[4 * q + 3] = v.w;
+        for (int q = 0; q < 8; q++) {
+          const float4 v = r4[q];
+          sp[2 * q] = (dct32::f2){v.x, v.y};
+          sp[2 * q + 1] = (dct32::f2){v.z, v.w};
+        }
+        dct32::dct2_32(sp, xp);
+        dct32::f2* w2 = reinterpret_cast<dct32::f2*>(row);
+#pragma unroll
+        for (int t = 0; t < 16; t++) w2[t] = xp[t];
       }
     }
-    const int mo = 2 * (k & 15) + (k >> 4);
-#pragma unroll
-    for (int third = 0; third < 3; third++) {
-      float ex[3], ey[3];
-#pragma unroll
-      for (int pp = 0; pp < 3; pp++) {
-        const int j = 6 * third + 2 * pp;
-        const float ox = xl::xor31(o[j]), oy = xl::xor31(o[j + 1]);
-        ex[pp] = k < 16 ? o[j] + ox : ox - o[j];
-        ey[pp] = k < 16 ? o[j + 1] + oy : oy - o[j + 1];
-      }
-      if (need_v && act) {
-        float ax[3][2], ay[3][2];
-#pragma unroll
-        for (int pp = 0; pp < 3; pp++) ax[pp][0] = ax[pp][1] = ay[pp][0] = ay[pp][1] = 0.0f;
-#pragma unroll
-        for (int pp = 0; pp < 3; pp++) {
-          ax[pp][0] = ex[pp] * dcp[0];
-          ay[pp][0] = ey[pp] * dcp[0];
-          xl::rot_fma15(ax[pp][0], ax[pp][1], ay[pp][0], ay[pp][1], ex[pp], ey[pp], dcp);
-        }
-#pragma unroll
-        for (int pp = 0; pp < 3; pp++) {
-          s.ring[ch][kHist + 6 * third + 2 * pp][mo] = ax[pp][0] + ax[pp][1];
-          s.ring[ch][kHist + 6 * third + 2 * pp + 1][mo] = ay[pp][0] + ay[pp][1];
-        }
-      }
-      if (third) stamp(3 + third);
-    }
+    stamp(5);
     wave_sync();  // ring slots of this granule written before the window reads them
 
     // ---- next granule in: raw/eo (dead after the matrixing) and the
@@ -636,28 +638,27 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
           dw[4 * q + 3] = v.w;
         }
       }
-      // taps (2t, 2t+1) of output ss read X_u[a] and X_{u-1}[b], u = ss - 2t:
-      // one pair P_u per u feeds up to 8 outputs as packed FMAs.  Two passes of
-      // 9 outputs keep the live pairs + accumulators within the register budget.
-      float acc[18];
+      // accumulator pair p = output slots (2p, 2p+1).  Tap 2t of the pair reads
+      // column a of rows (v, v+1) and tap 2t+1 column b of rows (v-1, v),
+      // v = 2p - 2t: every operand pair is two rows of one column, i.e. one
+      // ds_read2_b32 that lands as the packed operand, and each feeds up to 8
+      // accumulator pairs.
       const float* R = &s.ring[ch][0][0];
-      constexpr int kOut = 18 / kWinPasses;  // outputs per pass
+      f2 acc2[9];
 #pragma unroll
-      for (int pass = 0; pass < kWinPasses; pass++) {
-        f2 acc2[kOut];
+      for (int p = 0; p < 9; p++) acc2[p] = bcast(0.0f);
 #pragma unroll
-        for (int i = 0; i < kOut; i++) acc2[i] = bcast(0.0f);
+      for (int v = -14; v <= 16; v += 2) {
+        const f2 A = {R[(kHist + v) * kRow + pa], R[(kHist + v + 1) * kRow + pa]};
+        const f2 B = {R[(kHist + v - 1) * kRow + pb], R[(kHist + v) * kRow + pb]};
 #pragma unroll
-        for (int u = kOut * pass - 14; u < kOut * pass + kOut; u++) {
-          const f2 P = {R[(kHist + u) * 32 + ia], R[(kHist + u - 1) * 32 + ib]};
-#pragma unroll
-          for (int t = 0; t < 8; t++) {
-            const int i = u + 2 * t - kOut * pass;
-            if (i >= 0 && i < kOut) acc2[i] = pfma((f2){dw[2 * t], dw[2 * t + 1]}, P, acc2[i]);
+        for (int t = 0; t < 8; t++) {
+          const int p = v / 2 + t;
+          if (p >= 0 && p < 9) {
+            acc2[p] = pfma(bcast(dw[2 * t]), A, acc2[p]);
+            acc2[p] = pfma(bcast(dw[2 * t + 1]), B, acc2[p]);
           }
         }
-#pragma unroll
-        for (int i = 0; i < kOut; i++) acc[kOut * pass + i] = acc2[i].x + acc2[i].y;
       }
       // (L, R) sample pairs without LDS staging: one v_permlane32_swap per slot
       // pair hands lane i slot 2p's (L, R) and lane 32 + i slot 2p + 1's, so
@@ -666,8 +667,8 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       // lane 32 + i its slot 2p + 1, stored in both halves (frame.go:671-678).
 #pragma unroll
       for (int p = 0; p < 9; p++) {
-        const int a = (int)__builtin_amdgcn_fmed3f(acc[2 * p], -32767.0f, 32767.0f);
-        const int b = (int)__builtin_amdgcn_fmed3f(acc[2 * p + 1], -32767.0f, 32767.0f);
+        const int a = (int)__builtin_amdgcn_fmed3f(acc2[p].x, -32767.0f, 32767.0f);
+        const int b = (int)__builtin_amdgcn_fmed3f(acc2[p].y, -32767.0f, 32767.0f);
         const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
         pk[p] = ((uint32_t)r[0] & 0xffffu) | ((uint32_t)(nch == 2 ? r[1] : r[0]) << 16);
       }
@@ -677,8 +678,8 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     stamp(6);
 
     // ---- history shift (channels this granule touched) ----
-    for (int e = lane; e < nch * (kHist * 8); e += kLanes) {
-      const int c = e / (kHist * 8), r4 = e % (kHist * 8);
+    for (int e = lane; e < nch * (kHist * kRow / 4); e += kLanes) {
+      const int c = e / (kHist * kRow / 4), r4 = e % (kHist * kRow / 4);
       reinterpret_cast<float4*>(&s.ring[c][0][0])[r4] = reinterpret_cast<const float4*>(&s.ring[c][18][0])[r4];
     }
     wave_sync();

@@ -452,8 +452,8 @@ class Plan:
                                        p(d_state_out), p(d_pcm),
                                        C.c_void_p(stream) if stream else None))
 
-    PHASES = ("params", "requantize", "stereo+antialias", "imdct", "fold+matrix[0:9]",
-              "fold+matrix[9:18]", "window+store", "history")
+    PHASES = ("params", "requantize", "stereo+antialias", "imdct", "S rows (transpose)",
+              "dct32 (matrixing)", "window+store", "history")
 
     def debug_phases(self, d_gran, d_coef, d_pcm, stream=None):
         """Diagnostic (fast plans): summed shader cycles per kernel phase."""
