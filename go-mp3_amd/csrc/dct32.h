@@ -23,20 +23,22 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "pk.h"
+
 namespace mp3g {
 namespace dct32 {
 
-typedef float f2 __attribute__((ext_vector_type(2)));
+using pk::blo;
+using pk::bhi;
+using pk::f2;
+using pk::fma2;
+using pk::mk;
+using pk::mulmi;
+using pk::post_tw;
+using pk::pre_tw;
+using pk::swp;
 
 #define MP3G_D32 __host__ __device__ __forceinline__
-
-MP3G_D32 f2 mk(float a, float b) { return (f2){a, b}; }
-MP3G_D32 f2 swp(f2 v) { return __builtin_shufflevector(v, v, 1, 0); }
-MP3G_D32 f2 blo(f2 v) { return __builtin_shufflevector(v, v, 0, 0); }
-MP3G_D32 f2 bhi(f2 v) { return __builtin_shufflevector(v, v, 1, 1); }
-MP3G_D32 f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
-// (-i) * (x + iy) = y - ix
-MP3G_D32 f2 mulmi(f2 v) { return mk(v.y, -v.x); }
 
 // m of the two values of output pair t
 constexpr int kPairM[16][2] = {{1, 31},  {5, 27},  {9, 23},  {13, 19}, {17, 15}, {21, 11}, {25, 7},  {29, 3},
@@ -67,11 +69,6 @@ constexpr float kC4[4][4] = {{9.807852804e-01f, 8.314696123e-01f, 5.555702330e-0
 constexpr float kR2 = 7.071067812e-01f;   // cos(pi/4)
 constexpr float kC1 = 9.238795325e-01f;   // cos(pi/8)
 constexpr float kC3 = 3.826834324e-01f;   // cos(3 pi/8)
-
-// pre-twiddle: (a + ib) e^{-i theta} = a (c, -s) + b (s, c)
-MP3G_D32 f2 pre_tw(float a, float b, float c, float s) { return fma2(mk(b, b), mk(s, c), mk(a, a) * mk(c, -s)); }
-// post-twiddle, leaving (Re, -Im) of v e^{-i theta} = vr (c, s) + vi (s, -c)
-MP3G_D32 f2 post_tw(f2 v, float c, float s) { return fma2(bhi(v), mk(s, -c), blo(v) * mk(c, s)); }
 
 // in-place 4-point complex FFT (forward) of z0..z3
 MP3G_D32 void fft4(f2& z0, f2& z1, f2& z2, f2& z3) {

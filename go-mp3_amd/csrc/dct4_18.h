@@ -12,6 +12,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "pk.h"
+
 namespace mp3g {
 namespace dct4 {
 
@@ -80,6 +82,31 @@ __host__ __device__ __forceinline__ void dct4_18(const float x[18], float X[18])
     X[2 * k] = __builtin_fmaf(yr, c, yi * s);
     X[17 - 2 * k] = __builtin_fmaf(yr, s, -yi * c);
   }
+}
+
+// The same transform on packed float pairs (pk.h; ~80 v_pk_* instead of ~160
+// scalar operations): P[k] = (X[2k], X[17-2k]), k = 0..8.
+__host__ __device__ __forceinline__ void dft3p(pk::f2& a, pk::f2& b, pk::f2& c) {
+  const pk::f2 s = b + c, d = pk::mulmi(b - c);  // (b - c) * (-i)
+  const pk::f2 t = pk::fma2(pk::mk(-0.5f, -0.5f), s, a);
+  a += s;
+  b = pk::fma2(pk::mk(kH, kH), d, t);
+  c = pk::fma2(pk::mk(-kH, -kH), d, t);
+}
+__host__ __device__ __forceinline__ void dct4_18_pk(const float x[18], pk::f2 P[9]) {
+  pk::f2 z[9];
+#pragma unroll
+  for (int n = 0; n < 9; n++) z[n] = pk::pre_tw(x[2 * n], x[17 - 2 * n], kPre[n][0], kPre[n][1]);
+#pragma unroll
+  for (int n2 = 0; n2 < 3; n2++) dft3p(z[n2], z[3 + n2], z[6 + n2]);
+  z[4] = pk::cmul(z[4], kW[0][0], kW[0][1]);
+  z[7] = pk::cmul(z[7], kW[1][0], kW[1][1]);
+  z[5] = pk::cmul(z[5], kW[1][0], kW[1][1]);
+  z[8] = pk::cmul(z[8], kW[2][0], kW[2][1]);
+#pragma unroll
+  for (int k1 = 0; k1 < 3; k1++) dft3p(z[3 * k1], z[3 * k1 + 1], z[3 * k1 + 2]);
+#pragma unroll
+  for (int k = 0; k < 9; k++) P[k] = pk::post_tw(z[3 * (k % 3) + k / 3], kPost[k][0], kPost[k][1]);
 }
 
 // Short blocks (imdct.go:88-94): the 12-point IMDCT of each window as a

@@ -4,18 +4,11 @@
 // float32 multiplications, so the fast mode keeps them identical to the
 // reference (internal/frame/frame.go:140-420).
 // (compiled as part of kernels.hip)
+#include "granule_hdr.h"
+
 namespace mp3g {
 namespace common {
 
-__device__ __forceinline__ int hdr_mode(uint32_t h) { return (int)((h >> 6) & 3u); }
-__device__ __forceinline__ int hdr_nch(uint32_t h) { return hdr_mode(h) == 3 ? 1 : 2; }
-// line-table combination: lsf * 3 + sampling-frequency index (consts.go:68-97)
-__device__ __forceinline__ int hdr_combo(uint32_t h) {
-  const int lsf = ((h >> 19) & 3u) == 3u ? 0 : 1;
-  int sf = (int)((h >> 10) & 3u);
-  sf = sf > 2 ? 2 : sf;
-  return lsf * 3 + sf;
-}
 
 // int(sum * 32767) clamped to [-32767, 32767] (frame.go:663-669); Go's
 // out-of-range float->int conversion yields INT64_MIN -> -32767.

@@ -50,7 +50,7 @@ constexpr int kLanes = 64;
 // Packed FP32: one v_pk_fma_f32 does two FMAs in the issue slot of one
 // v_fma_f32 (measured on MI355X: 122 vs 51-69 TFLOP/s, tools/valu_bench.hip),
 // so the IMDCT, matrixing and window sums are written on float pairs.
-typedef float f2 __attribute__((ext_vector_type(2)));
+using pk::f2;
 __device__ __forceinline__ f2 pfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ __forceinline__ f2 bcast(float v) { return (f2){v, v}; }
 // pretab[22] (frame.go:39) packed 2 bits per band: no per-lane table load
@@ -74,7 +74,11 @@ constexpr int kWinPasses = MP3G_WIN_PASSES;
 
 // read-only tables, one copy per workgroup
 struct __align__(16) SharedSmem {
-  float win[4][36];    // imdctWinData
+  // imdctWinData (imdct.go:21-57) per block type and subband parity as
+  // (Wp, Wn) pairs per q = 0..8 (see the IMDCT): Wp = (W[q], -W[17-q]),
+  // Wn = (-W[18+q], -W[35-q]), each element times the frequency-inversion
+  // sign of its line in an odd subband (frame.go:480-486)
+  float4 winp[4][2][9];
   float isr[8][2];
   float dwin[32][16];  // FastTables::dwin rows, pre-scaled by 32767
   // FastTables::lband: read per lane every granule, so it lives in LDS -- a
@@ -94,7 +98,7 @@ struct __align__(16) WaveSmem {
   // them into X in place
   float ring[2][kRing][kRow];
   // requantization exponents n4 of the long bands [ch][sfb] and short bands [ch][sfb][win]
-  int expo[2 * 22 + 2 * 39];
+  int16_t expo[2 * 22 + 2 * 39];
   mp3g_granule desc;
 };
 
@@ -224,7 +228,13 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
   __shared__ WaveSmem wsm[kWaves];
   {
     const int t = threadIdx.x;
-    for (int e = t; e < 4 * 36; e += kLanes * kWaves) (&sh.win[0][0])[e] = (&g_fast.win[0][0])[e];
+    for (int e = t; e < 4 * 2 * 9; e += kLanes * kWaves) {
+      const int bt = e / 18, par = (e / 9) & 1, q = e % 9;
+      const float* W = g_fast.win[bt];
+      // frequency inversion: line j of an odd subband is negated when j is odd
+      const float sq = par && (q & 1) ? -1.0f : 1.0f, sr = par && !(q & 1) ? -1.0f : 1.0f;  // j = q, 17 - q
+      sh.winp[bt][par][q] = make_float4(W[q] * sq, -W[17 - q] * sr, -W[18 + q] * sq, -W[35 - q] * sr);
+    }
     for (int e = t; e < 16; e += kLanes * kWaves) (&sh.isr[0][0])[e] = (&g_fast.is_ratio[0][0])[e];
     for (int e = t; e < 32 * 16; e += kLanes * kWaves) (&sh.dwin[0][0])[e] = (&g_fast.dwin[0][0])[e] * 32767.0f;
     for (int e = t; e < kCombos * 32; e += kLanes * kWaves) (&sh.lband[0][0])[e] = (&g_fast.lband[0][0])[e];
@@ -254,13 +264,21 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
   const mp3g_state* sin = state_in ? state_in + cd.stream : nullptr;
 
   // entry state: overlap store in registers, V history as X vectors
-  float st[18];
+  // IMDCT overlap `store` (frame.go:473-476) in registers as pairs
+  // stp[q] = (store[q], store[17-q]), each element times the frequency-inversion
+  // sign of its line (odd line of an odd subband: -1), so the overlap-add
+  // yields frequency-inverted output directly
+  const float sodd = (k & 1) ? -1.0f : 1.0f;  // sign of the odd lines of this subband
+  f2 stp[9];
   {
     // (no dynamic indexing of init_in[]: a private array would be promoted to LDS)
     const bool in0 = init_in[0] && sin, in1 = init_in[1] && sin;
     const bool from_in = ch ? in1 : in0;
 #pragma unroll
-    for (int j = 0; j < 18; j++) st[j] = from_in ? sin->store[ch][k][j] : 0.0f;
+    for (int q = 0; q < 9; q++) {
+      const float a = from_in ? sin->store[ch][k][q] : 0.0f, b = from_in ? sin->store[ch][k][17 - q] : 0.0f;
+      stp[q] = (f2){(q & 1) ? a * sodd : a, (q & 1) ? b : b * sodd};
+    }
     for (int e = lane; e < 2 * kHist * 32; e += kLanes) {
       const int c = e / (kHist * 32), blk = (e >> 5) % kHist, m = e & 31;
       const bool in = c ? in1 : in0;
@@ -510,8 +528,15 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       int bt = C.block_type & 3;
       if (C.win_switch_flag == 1 && C.mixed_block_flag == 1 && k < 2) bt = 0;
       // raw[0..17] + old overlap -> o[], raw[18..35] -> new overlap, written as
-      // each raw value is produced (no 36-entry temporary)
+      // each raw value is produced (no 36-entry temporary); frequency
+      // inversion rides on the signs of the windows and of stp
       if (bt == 2) {
+        float st[18];
+#pragma unroll
+        for (int q = 0; q < 9; q++) {
+          st[q] = stp[q].x;
+          st[17 - q] = stp[q].y;
+        }
         // raw[pos] = sum over the windows wi with 0 <= pos-6-6wi < 12 of
         // (sum_m x[wi+3m] cosN12[m][p]) * win[2][p], p = pos-6-6wi (imdct.go:88-94)
 #pragma unroll
@@ -526,26 +551,34 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
             for (int m = 0; m < 6; m++) sum += x[wi + 3 * m] * dct4::kCos12[p][m];
             raw += sum * dct4::kWin12[p];
           }
+          if (pos & 1) raw *= sodd;  // (pos and pos - 18 have the same parity)
           if (pos < 18) o[pos] = raw + st[pos];
           else st[pos - 18] = self(act, raw, st[pos - 18]);
         }
-      } else {
-        const float* W = sh.win[bt];
-        // the 18 distinct sums are a DCT-IV of size 18 (dct4_18.h):
-        // sum_m x[m] cosN36[m][q] = X[9+q], sum_m x[m] cosN36[m][18+q] = -X[8-q]
-        float X[18];
-        dct4::dct4_18(x, X);
 #pragma unroll
-        for (int q = 0; q < 9; q++) {
-          const float za = X[9 + q], zb = -X[8 - q];
-          o[q] = za * W[q] + st[q];
-          o[17 - q] = -za * W[17 - q] + st[17 - q];
-          st[q] = self(act, zb * W[18 + q], st[q]);
-          st[17 - q] = self(act, zb * W[35 - q], st[17 - q]);
+        for (int q = 0; q < 9; q++) stp[q] = (f2){st[q], st[17 - q]};
+      } else {
+        // the 18 distinct sums are a DCT-IV of size 18 (dct4_18.h):
+        // sum_m x[m] cosN36[m][q] = X[9+q], sum_m x[m] cosN36[m][18+q] = -X[8-q];
+        // packed, pair k = (X[2k], X[17-2k]) holds X[9+q] and X[8-q] of one q
+        f2 P[9];
+        dct4::dct4_18_pk(x, P);
+        const float4* Wq = sh.winp[bt][k & 1];
+#pragma unroll
+        for (int kk = 0; kk < 9; kk++) {
+          const int q = kk <= 4 ? 8 - 2 * kk : 2 * kk - 9;
+          const float za = kk <= 4 ? P[kk].y : P[kk].x;  // X[9+q]
+          const float zb = kk <= 4 ? P[kk].x : P[kk].y;  // X[8-q]
+          const float4 w = Wq[q];
+          // (o[q], o[17-q]) = X[9+q] (W[q], -W[17-q]) + stp[q];
+          // new stp[q] = X[8-q] (-W[18+q], -W[35-q])   (signs folded in w)
+          const f2 oq = pfma(bcast(za), (f2){w.x, w.y}, stp[q]);
+          o[q] = oq.x;
+          o[17 - q] = oq.y;
+          const f2 ns = bcast(zb) * (f2){w.z, w.w};
+          stp[q] = (f2){self(act, ns.x, stp[q].x), self(act, ns.y, stp[q].y)};
         }
       }
-#pragma unroll
-      for (int j = 1; j < 18; j += 2) o[j] = self(k & 1, -o[j], o[j]);  // frequency inversion
     }
     wave_sync();  // raw[] fully consumed before eo[] (same LDS) is written
     stamp(3);
@@ -691,7 +724,10 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
   if (cd.flags & kChunkStateOut) {
     mp3g_state* so = state_out + cd.stream;
 #pragma unroll
-    for (int j = 0; j < 18; j++) so->store[ch][k][j] = st[j];
+    for (int q = 0; q < 9; q++) {
+      so->store[ch][k][q] = (q & 1) ? stp[q].x * sodd : stp[q].x;
+      so->store[ch][k][17 - q] = (q & 1) ? stp[q].y : stp[q].y * sodd;
+    }
     for (int e = lane; e < 2 * 1024; e += kLanes) {
       const int c = e >> 10, blk = (e >> 6) & 15, i = e & 63;
       so->vvec[c][64 * blk + i] = blk < kHist ? v_from_x(s.ring[c][kHist - 1 - blk], i) : 0.0f;

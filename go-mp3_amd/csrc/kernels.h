@@ -55,4 +55,12 @@ hipError_t launch_fast_stamped(const ChunkDesc* d_chunks, uint32_t n_chunks, con
                                const int16_t* d_coef, const mp3g_state* d_state_in, mp3g_state* d_state_out,
                                int16_t* d_pcm, unsigned long long* d_stamps, hipStream_t stream);
 
+// The fast kernel's TU (kernels_fast.hip): its table copy, attributes and launch
+// (d_stamps = nullptr: the production build).
+hipError_t upload_fast_tables(const FastTables& fast);
+hipError_t fast_kernel_attributes(hipFuncAttributes* a, int* waves_per_block);
+hipError_t launch_fast(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_granule* d_gran,
+                       const int16_t* d_coef, const mp3g_state* d_state_in, mp3g_state* d_state_out,
+                       int16_t* d_pcm, unsigned long long* d_stamps, hipStream_t stream);
+
 }  // namespace mp3g

@@ -1,11 +1,13 @@
-// kernels.hip -- the single device translation unit of libmp3g.so.
+// kernels.hip -- device translation unit of the exact-mode and main-data
+// kernels of libmp3g.so.
 //
-// Holds the constant tables (uploaded once per device) and both exact-mode
+// Holds their constant tables (uploaded once per device) and both exact-mode
 // kernels: v1 (granule_exact.hip, the straightforward per-phase version, kept
 // as an on-device cross-check) and v2 (granule_fused.hip, the production
-// kernel), the fast-mode kernel v3 (granule_fast.hip, +-1 LSB) and the
-// main-data (scale factor + Huffman) kernel (huffman_dev.hip).  One TU
-// so all of them reach g_tab / g_fast / g_huff without relocatable device code.
+// kernel), and the main-data (scale factor + Huffman) kernel
+// (huffman_dev.hip).  One TU so they reach g_tab / g_huff without
+// relocatable device code.  The fast-mode kernel v3 has a TU of its own
+// (kernels_fast.hip: its own table copy g_fast and codegen options).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -18,14 +20,12 @@
 
 namespace mp3g {
 __device__ DspTables g_tab;
-__constant__ FastTables g_fast;
 __device__ HuffLut g_huff;
 }  // namespace mp3g
 
 #include "granule_common.hip"
 #include "granule_exact.hip"
 #include "granule_fused.hip"
-#include "granule_fast.hip"
 #include "huffman_dev.hip"
 
 namespace mp3g {
@@ -35,7 +35,7 @@ hipError_t upload_tables(const DspTables& tables) {
   if (e != hipSuccess) return e;
   FastTables fast;
   build_fast_tables(tables, &fast);
-  e = hipMemcpyToSymbol(HIP_SYMBOL(g_fast), &fast, sizeof(FastTables), 0, hipMemcpyHostToDevice);
+  e = upload_fast_tables(fast);
   if (e != hipSuccess) return e;
   HuffLut* lut = new HuffLut;
   if (!build_huff_lut(lut)) {
@@ -52,8 +52,7 @@ int chunks_per_cu(int variant) {
   hipError_t e;
   int waves_per_block;
   if (variant == kVariantFast) {
-    e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&v3::granule_fast_kernel<false>));
-    waves_per_block = v3::kWaves;
+    e = fast_kernel_attributes(&a, &waves_per_block);
   } else if (variant == kVariantV1) {
     e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&v1::granule_exact_kernel));
     waves_per_block = 4;
@@ -78,25 +77,13 @@ hipError_t launch_granule(int variant, const ChunkDesc* d_chunks, uint32_t n_chu
                           hipStream_t stream) {
   if (n_chunks == 0) return hipSuccess;
   if (variant == kVariantFast)
-    hipLaunchKernelGGL(v3::granule_fast_kernel<false>, dim3((n_chunks + v3::kWaves - 1) / v3::kWaves),
-                       dim3(64 * v3::kWaves), 0, stream, d_chunks, n_chunks, d_gran, d_coef, d_state_in,
-                       d_state_out, d_pcm, nullptr);
+    return launch_fast(d_chunks, n_chunks, d_gran, d_coef, d_state_in, d_state_out, d_pcm, nullptr, stream);
   else if (variant == kVariantV1)
     hipLaunchKernelGGL(v1::granule_exact_kernel, dim3(n_chunks), dim3(256), 0, stream, d_chunks,
                        d_gran, d_coef, d_state_in, d_state_out, d_pcm);
   else
     hipLaunchKernelGGL(v2::granule_fused_kernel, dim3(n_chunks), dim3(256), 0, stream, d_chunks,
                        d_gran, d_coef, d_state_in, d_state_out, d_pcm);
-  return hipGetLastError();
-}
-
-hipError_t launch_fast_stamped(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_granule* d_gran,
-                               const int16_t* d_coef, const mp3g_state* d_state_in, mp3g_state* d_state_out,
-                               int16_t* d_pcm, unsigned long long* d_stamps, hipStream_t stream) {
-  if (n_chunks == 0) return hipSuccess;
-  hipLaunchKernelGGL(v3::granule_fast_kernel<true>, dim3((n_chunks + v3::kWaves - 1) / v3::kWaves),
-                     dim3(64 * v3::kWaves), 0, stream, d_chunks, n_chunks, d_gran, d_coef, d_state_in, d_state_out,
-                     d_pcm, d_stamps);
   return hipGetLastError();
 }
 

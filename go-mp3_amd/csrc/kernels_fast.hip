@@ -1,0 +1,58 @@
+// kernels_fast.hip -- device translation unit of the fast-mode granule kernel
+// (v3, granule_fast.hip, MP3G_MODE_FAST) with its own copy of the fast tables.
+//
+// Own TU so it gets its own codegen options (Makefile): it is compiled with
+// machine LICM off.  The kernel's packed-FP32 transforms take their constants
+// from SGPR pairs (VOP3P has no literal operand); hoisted out of the granule
+// loop, ~90 of them overflow the wave's SGPRs and were spilled to VGPR lanes,
+// costing a v_readlane (VALU) per use inside the loop.  Left in place they are
+// s_mov_b32 (SALU) next to their use.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "../../include/mp3g.h"
+#include "dsp_tables.h"
+#include "kernels.h"
+
+#pragma clang fp contract(off)
+
+namespace mp3g {
+__constant__ FastTables g_fast;
+}  // namespace mp3g
+
+#include "granule_hdr.h"
+#include "granule_fast.hip"
+
+namespace mp3g {
+
+hipError_t upload_fast_tables(const FastTables& fast) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_fast), &fast, sizeof(FastTables), 0, hipMemcpyHostToDevice);
+}
+
+hipError_t fast_kernel_attributes(hipFuncAttributes* a, int* waves_per_block) {
+  *waves_per_block = v3::kWaves;
+  return hipFuncGetAttributes(a, reinterpret_cast<const void*>(&v3::granule_fast_kernel<false>));
+}
+
+hipError_t launch_fast(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_granule* d_gran,
+                       const int16_t* d_coef, const mp3g_state* d_state_in, mp3g_state* d_state_out,
+                       int16_t* d_pcm, unsigned long long* d_stamps, hipStream_t stream) {
+  if (n_chunks == 0) return hipSuccess;
+  const dim3 grid((n_chunks + v3::kWaves - 1) / v3::kWaves), block(64 * v3::kWaves);
+  if (d_stamps)
+    hipLaunchKernelGGL(v3::granule_fast_kernel<true>, grid, block, 0, stream, d_chunks, n_chunks, d_gran, d_coef,
+                       d_state_in, d_state_out, d_pcm, d_stamps);
+  else
+    hipLaunchKernelGGL(v3::granule_fast_kernel<false>, grid, block, 0, stream, d_chunks, n_chunks, d_gran, d_coef,
+                       d_state_in, d_state_out, d_pcm, nullptr);
+  return hipGetLastError();
+}
+
+hipError_t launch_fast_stamped(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_granule* d_gran,
+                               const int16_t* d_coef, const mp3g_state* d_state_in, mp3g_state* d_state_out,
+                               int16_t* d_pcm, unsigned long long* d_stamps, hipStream_t stream) {
+  return launch_fast(d_chunks, n_chunks, d_gran, d_coef, d_state_in, d_state_out, d_pcm, d_stamps, stream);
+}
+
+}  // namespace mp3g

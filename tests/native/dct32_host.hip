@@ -23,3 +23,18 @@ extern "C" void dct32_tables(int* pair_m, int* pos_of_m) {
   for (int t = 0; t < 32; t++) pair_m[t] = mp3g::dct32::kPairM[t / 2][t % 2];
   for (int m = 0; m < 32; m++) pos_of_m[m] = mp3g::dct32::kPosOfM[m];
 }
+
+#include "../../go-mp3_amd/csrc/dct4_18.h"
+
+// x[n][18] -> X[n][18]: the scalar and the packed DCT-IV-18 of the IMDCT
+extern "C" void dct4_18_host(const float* x, float* X, float* Xp, int n) {
+  for (int i = 0; i < n; i++) {
+    mp3g::dct4::dct4_18(x + 18 * i, X + 18 * i);
+    mp3g::pk::f2 P[9];
+    mp3g::dct4::dct4_18_pk(x + 18 * i, P);
+    for (int k = 0; k < 9; k++) {
+      Xp[18 * i + 2 * k] = P[k].x;
+      Xp[18 * i + 17 - 2 * k] = P[k].y;
+    }
+  }
+}

@@ -120,9 +120,10 @@ def test_exact_kernel_has_no_fma():
     """Exact mode contract: no fused multiply-add in the device code
     (Go on linux/amd64 rounds every float32 product and sum)."""
     csrc = os.path.join(REPO, "go-mp3_amd", "csrc")
-    subprocess.check_call(["make", "-s", "-C", csrc, "build/kernels.s"],
+    subprocess.check_call(["make", "-s", "-C", csrc, "build/kernels.s", "build/kernels_fast.s"],
                           stderr=subprocess.DEVNULL)
-    asm = open(os.path.join(csrc, "build", "kernels.s")).read()
+    asm = open(os.path.join(csrc, "build", "kernels.s")).read() + \
+        open(os.path.join(csrc, "build", "kernels_fast.s")).read()
     kernels = re.findall(r"^(_ZN4mp3g2v\d\w+kernel\w*):(.*?)\.end_amdhsa_kernel", asm, re.S | re.M)
     exact = [(n, b) for n, b in kernels if "granule_fast" not in n]
     fast = [(n, b) for n, b in kernels if "granule_fast" in n]

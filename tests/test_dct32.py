@@ -78,3 +78,20 @@ def test_dct32_matches_synth_nwin(lib):
     V[:, 48:] = -X[:, :16]
     want = S.astype(np.float64) @ nwin.T
     assert np.abs(V - want).max() < 2e-5
+
+
+def test_dct4_18_packed(lib):
+    """The IMDCT-36's DCT-IV-18 (dct4_18.h), scalar and packed forms, against
+    float64 X[k] = sum_m x[m] cos(pi/72 (2k+1)(2m+1))."""
+    lib.dct4_18_host.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+    rng = np.random.default_rng(8)
+    x = rng.standard_normal((2000, 18)).astype(np.float32)
+    X = np.empty_like(x)
+    Xp = np.empty_like(x)
+    lib.dct4_18_host(x.ctypes.data, X.ctypes.data, Xp.ctypes.data, len(x))
+    m = np.arange(18)
+    M = np.cos(np.pi / 72 * np.outer(2 * m + 1, 2 * m + 1))
+    want = x.astype(np.float64) @ M.T
+    l1 = np.abs(x.astype(np.float64)).sum(axis=1)
+    assert (np.abs(X - want).max(axis=1) / l1).max() < 4e-7
+    assert (np.abs(Xp - want).max(axis=1) / l1).max() < 4e-7
