@@ -108,8 +108,10 @@ MP3G_D32 void dct4_8(const f2 bp[4], f2 out[4]) {
 }
 
 // X[m] = sum_k S[k] cos(pi m (2k+1) / 64) for one slot.  sp[j] = (S[2j], S[2j+1]);
-// xp[t] = (X[kPairM[t][0]], X[kPairM[t][1]]).
-MP3G_D32 void dct2_32(const f2 sp[16], f2 xp[16]) {
+// out(t, xp) receives pair t = (X[kPairM[t][0]], X[kPairM[t][1]]) as soon as it
+// is computed (the caller stores it: fewer values live at once).
+template <class Out>
+MP3G_D32 void dct2_32_to(const f2 sp[16], Out out) {
   // fold 32 -> even part e (DCT2_16) and odd part d (DCT4_16)
   f2 ep[8], dp[8];
 #pragma unroll
@@ -118,7 +120,12 @@ MP3G_D32 void dct2_32(const f2 sp[16], f2 xp[16]) {
     ep[j] = sp[j] + r;
     dp[j] = sp[j] - r;
   }
-  dct4_16(dp, xp);  // pairs 0..7: m = 4k+1, 31-4k
+  {
+    f2 x4[8];
+    dct4_16(dp, x4);  // pairs 0..7: m = 4k+1, 31-4k
+#pragma unroll
+    for (int t = 0; t < 8; t++) out(t, x4[t]);
+  }
   // DCT2_16(e): fold -> a (DCT2_8), b (DCT4_8)
   f2 ap[4], bp[4];
 #pragma unroll
@@ -127,7 +134,12 @@ MP3G_D32 void dct2_32(const f2 sp[16], f2 xp[16]) {
     ap[j] = ep[j] + r;
     bp[j] = ep[j] - r;
   }
-  dct4_8(bp, xp + 8);  // pairs 8..11: m = 8k+2, 30-8k
+  {
+    f2 x8[4];
+    dct4_8(bp, x8);  // pairs 8..11: m = 8k+2, 30-8k
+#pragma unroll
+    for (int t = 0; t < 4; t++) out(8 + t, x8[t]);
+  }
   // DCT2_8(a): fold -> a' (DCT2_4), a'' (DCT4_4)
   const f2 r1 = swp(ap[3]), r0 = swp(ap[2]);
   const f2 a1p0 = ap[0] + r1, a1p1 = ap[1] + r0;  // a'[0..3] as pairs
@@ -142,14 +154,18 @@ MP3G_D32 void dct2_32(const f2 sp[16], f2 xp[16]) {
     y23 = fma2(blo(a2p1), mk(kC4[2][2], kC4[2][3]), y23);
     y01 = fma2(bhi(a2p1), mk(kC4[3][0], kC4[3][1]), y01);
     y23 = fma2(bhi(a2p1), mk(kC4[3][2], kC4[3][3]), y23);
-    xp[12] = y01;
-    xp[13] = y23;
+    out(12, y01);
+    out(13, y23);
   }
   // DCT2_4(a'): fold -> u (DCT2_2: m = 0, 16), w (DCT4_2: m = 8, 24)
   const f2 u = a1p0 + swp(a1p1);  // (a'0 + a'3, a'1 + a'2)
   const f2 w = a1p0 - swp(a1p1);  // (a'0 - a'3, a'1 - a'2)
-  xp[14] = (blo(u) + mk(u.y, -u.y)) * mk(1.0f, kR2);
-  xp[15] = fma2(bhi(w), mk(kC3, -kC1), blo(w) * mk(kC1, kC3));
+  out(14, (blo(u) + mk(u.y, -u.y)) * mk(1.0f, kR2));
+  out(15, fma2(bhi(w), mk(kC3, -kC1), blo(w) * mk(kC1, kC3)));
+}
+
+MP3G_D32 void dct2_32(const f2 sp[16], f2 xp[16]) {
+  dct2_32_to(sp, [&](int t, f2 v) { xp[t] = v; });
 }
 
 }  // namespace dct32

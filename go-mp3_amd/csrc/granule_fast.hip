@@ -55,22 +55,28 @@ __device__ __forceinline__ f2 pfma(f2 a, f2 b, f2 c) { return __builtin_elementw
 __device__ __forceinline__ f2 bcast(float v) { return (f2){v, v}; }
 // pretab[22] (frame.go:39) packed 2 bits per band: no per-lane table load
 __device__ __forceinline__ int kPretab(int sfb) { return (int)((0x2fe95400000ull >> (2 * sfb)) & 3u); }
-// X ring slots: 0..14 history (slot 14 newest), 15..32 the current granule.
-// The window of slot ss reads slots 15+ss-j, j = 0..15, so 15 history slots
+// The X ring, column-major: ring[ch][m][u] = X_u[m], the value m (in
+// dct32::kPosOfM order) of time slot u.  Slots 1..15 hold the previous
+// granule's last 15 slots (slot 0 is unused), 16..33 the current granule; the
+// window of slot ss reads slots 16+ss-j, j = 0..15, so 15 history slots
 // suffice (the 16th V block of Frame.vVec is never read again).
-constexpr int kHist = 15;
-constexpr int kRing = kHist + 18;
-// ring row: 32 values + 4 of padding.  144-B rows keep the row-per-lane
-// accesses of the matrixing (16-B reads, 8-B writes by lanes of different
-// rows) free of bank conflicts.
-constexpr int kRow = 36;
-// window passes per granule: each X pair feeds up to 8 outputs; one pass of 18
-// outputs reads every pair once (64 LDS reads), two passes of 9 re-read the
-// 14 shared pairs (92) but hold half the accumulators
-#ifndef MP3G_WIN_PASSES
-#define MP3G_WIN_PASSES 1
+//  * every operand pair of the window is two consecutive slots of one column:
+//    (16+v, 17+v), v even, is one 8-B aligned ds_read_b64, (15+v, 16+v) one
+//    ds_read2_b32;
+//  * 34 dwords per column (34 = 2 mod 32): the columns the 32 lanes of a
+//    channel read start in distinct even banks (conflict-free b64 reads);
+//  * the matrixing lane of slot u reads and writes its slot across the 32
+//    columns: consecutive lanes hit consecutive dwords;
+//  * 2 x 32 x 34 x 4 = 8,704 B per wave, which with the raw coefficients in
+//    registers (no LDS copy) brings a 4-wave workgroup to 40.5 KB: 4
+//    workgroups = 16 waves per CU.
+constexpr int kHist = 16;
+// 4 workgroups of 4 waves per CU: <= 128 VGPRs (MI355X_MICROARCH.md register
+// table) next to the 40.5 KB of LDS per workgroup
+#ifndef MP3G_FAST_WAVES_PER_SIMD
+#define MP3G_FAST_WAVES_PER_SIMD 4
 #endif
-constexpr int kWinPasses = MP3G_WIN_PASSES;
+constexpr int kSlots = kHist + 18;
 
 // read-only tables, one copy per workgroup
 struct __align__(16) SharedSmem {
@@ -86,30 +92,35 @@ struct __align__(16) SharedSmem {
   // granule's PCM stores
   uint32_t lband[kCombos][32];
 };
-// per-wave working set ~11.9 KB.  The workgroup (4 waves + shared tables) must
-// stay <= 42 x 1280 B (gfx950 LDS allocation granule) for 3 workgroups
-// (12 waves) per CU.
+// per-wave working set 9.1 KB.  The workgroup (4 waves + shared tables) must
+// stay <= 32 x 1280 B (gfx950 LDS allocation granule) for 4 workgroups
+// (16 waves) per CU.
 struct __align__(16) WaveSmem {
-  union {
-    int16_t raw[2][576];  // Huffman integers of the current granule
-  } a;
-  // X vectors in dct32::kPosOfM order; the current granule's rows first
-  // receive S (the IMDCT output, one row per slot) and the matrixing turns
-  // them into X in place
-  float ring[2][kRing][kRow];
+  // the current granule's slots of a column (16..33) first receive S (the
+  // IMDCT output of subband k = column, one value per slot) and the matrixing
+  // turns them into X in place; before that they stage the raw coefficients
+  // of short-block granules (reorder gather) and the intensity-stereo pass
+  float ring[2][32][kSlots];
   // requantization exponents n4 of the long bands [ch][sfb] and short bands [ch][sfb][win]
   int16_t expo[2 * 22 + 2 * 39];
   mp3g_granule desc;
 };
 
-__device__ __forceinline__ void load_granule(WaveSmem& s, const mp3g_granule* gran, const int16_t* coef,
-                                             uint64_t g, int t) {
-  const uint4* src = reinterpret_cast<const uint4*>(coef + g * MP3G_COEF_PER_GRANULE);
-  uint4* dst = reinterpret_cast<uint4*>(&s.a.raw[0][0]);
-  dst[t] = src[t];
-  dst[t + 64] = src[t + 64];
-  if (t < 16) dst[t + 128] = src[t + 128];
-  if (t < 10) reinterpret_cast<uint4*>(&s.desc)[t] = reinterpret_cast<const uint4*>(gran + g)[t];
+// Raw coefficients of lane (ch, sb) of granule g: its 18 lines, 36 B at
+// coef[g][ch][18 sb], as 9 dwords (two int16 each) by three 12-B buffer loads
+// through a per-granule resource (SGPR base, 32-bit lane offset).
+__device__ __forceinline__ void load_lines(const int16_t* coef, uint32_t g, int lane, uint32_t cw[9]) {
+  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<int16_t*>(coef + (size_t)g * MP3G_COEF_PER_GRANULE), (short)0,
+      (int)(MP3G_COEF_PER_GRANULE * sizeof(int16_t)), 0x00020000);
+  const int off = (lane >> 5) * 1152 + (lane & 31) * 36;
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b96(rc, off + 12 * i, 0, 0);
+    cw[3 * i] = v[0];
+    cw[3 * i + 1] = v[1];
+    cw[3 * i + 2] = v[2];
+  }
 }
 
 // Replay start of a chunk (same decision as v2::plan_prologue, with wave
@@ -193,15 +204,26 @@ __device__ __forceinline__ float requant_fast(int xi, int n4) {
   return copysignf(ldexpf(__builtin_amdgcn_exp2f(t), n4 >> 2), xf);
 }
 
+// The lane id, recomputed where it is used (asm volatile: not hoisted out of
+// the granule loop).  Values derived from it once and kept for the whole loop
+// cost a VGPR each; at the 128-VGPR budget the allocator spilled some to
+// scratch, and a reload is a VMEM load whose s_waitcnt also waits for the
+// in-flight PCM stores and prefetch.
+__device__ __forceinline__ int lane_fresh() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+
 // X of a V block: X[m] = V[m-16] (m >= 16), -V[48-m] (m < 16).
 __device__ __forceinline__ float x_from_v(const float* v, int m) { return m >= 16 ? v[m - 16] : -v[48 - m]; }
 // V of an X vector (inverse identity; V[16] = 0).
-// x holds X in dct32::kPosOfM order.
+// x: one slot of the column-major ring (X[m] at x[kSlots * kPosOfM[m]]).
 __device__ __forceinline__ float v_from_x(const float* x, int i) {
-  if (i < 16) return x[dct32::kPosOfM[16 + i]];
+  if (i < 16) return x[kSlots * dct32::kPosOfM[16 + i]];
   if (i == 16) return 0.0f;
-  if (i < 48) return -x[dct32::kPosOfM[48 - i]];
-  return -x[dct32::kPosOfM[i - 48]];
+  if (i < 48) return -x[kSlots * dct32::kPosOfM[48 - i]];
+  return -x[kSlots * dct32::kPosOfM[i - 48]];
 }
 
 }  // namespace
@@ -210,7 +232,7 @@ __device__ __forceinline__ float v_from_x(const float* x, int i) {
 // to `stamps` (kPhases per workgroup); never used for output.
 constexpr int kPhases = 8;
 template <bool kStamp>
-__global__ void __launch_bounds__(kLanes * kWaves, 3)
+__global__ void __launch_bounds__(kLanes * kWaves, MP3G_FAST_WAVES_PER_SIMD)
 granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, const mp3g_granule* __restrict__ gran,
                     const int16_t* __restrict__ coef, const mp3g_state* __restrict__ state_in,
                     mp3g_state* __restrict__ state_out, int16_t* __restrict__ pcm,
@@ -226,6 +248,12 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
   };
   __shared__ SharedSmem sh;
   __shared__ WaveSmem wsm[kWaves];
+#ifdef MP3G_FAST_LDS_PAD
+  // diagnostic builds only (tools/build_variant.sh): extra LDS per workgroup
+  // to lower the resident workgroups per CU (occupancy sensitivity)
+  __shared__ char ldspad[MP3G_FAST_LDS_PAD];
+  if (n_chunks == 0xffffffffu) reinterpret_cast<volatile char*>(ldspad)[threadIdx.x] = 0;
+#endif
   {
     const int t = threadIdx.x;
     for (int e = t; e < 4 * 2 * 9; e += kLanes * kWaves) {
@@ -279,14 +307,18 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       const float a = from_in ? sin->store[ch][k][q] : 0.0f, b = from_in ? sin->store[ch][k][17 - q] : 0.0f;
       stp[q] = (f2){(q & 1) ? a * sodd : a, (q & 1) ? b : b * sodd};
     }
-    for (int e = lane; e < 2 * kHist * 32; e += kLanes) {
-      const int c = e / (kHist * 32), blk = (e >> 5) % kHist, m = e & 31;
+    for (int e = lane; e < 2 * 15 * 32; e += kLanes) {
+      const int c = e / (15 * 32), blk = (e >> 5) % 15, m = e & 31;
       const bool in = c ? in1 : in0;
-      s.ring[c][kHist - 1 - blk][dct32::kPosOfM[m]] = in ? x_from_v(&sin->vvec[c][64 * blk], m) : 0.0f;
+      s.ring[c][dct32::kPosOfM[m]][kHist - 1 - blk] = in ? x_from_v(&sin->vvec[c][64 * blk], m) : 0.0f;
     }
   }
 
-  if (w < end) load_granule(s, gran, coef, w, lane);
+  uint32_t cw[9] = {};  // the current granule's raw coefficients (lane's 18 lines)
+  if (w < end) {
+    load_lines(coef, w, lane, cw);
+    if (lane < 10) reinterpret_cast<uint4*>(&s.desc)[lane] = reinterpret_cast<const uint4*>(gran + w)[lane];
+  }
   wave_sync();
 
   // PCM of a granule is stored during the next granule's front end: a VMEM
@@ -376,12 +408,10 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     float x[18];
     if (all_long) {
       int xi[18];
-      const uint32_t* rw = reinterpret_cast<const uint32_t*>(&s.a.raw[ch][18 * k]);
 #pragma unroll
       for (int q = 0; q < 9; q++) {
-        const uint32_t w = rw[q];
-        xi[2 * q] = (int)(int16_t)(w & 0xffffu);
-        xi[2 * q + 1] = (int)(int16_t)(w >> 16);
+        xi[2 * q] = (int)(int16_t)(cw[q] & 0xffffu);
+        xi[2 * q + 1] = (int)(int16_t)(cw[q] >> 16);
       }
       // long band of line j: first band of the subband + band starts among lines 1..j
       const uint32_t lb = sh.lband[combo][k];
@@ -396,11 +426,25 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
 #pragma unroll
       for (int j = 0; j < 18; j++) x[j] = requant_fast(xi[j], ex[j]);
     } else {
-      const uint32_t* li = &g_fast.linfo[combo][18 * k];
+      // reorder gather: the channel's raw lines staged in the current slots of
+      // the ring, lane (ch, sb) writing its 9 dwords to column sb
+      {
+        uint32_t* col = reinterpret_cast<uint32_t*>(&s.ring[ch][k][kHist]);
+#pragma unroll
+        for (int q = 0; q < 9; q++) col[q] = cw[q];
+      }
+      wave_sync();
+      const int16_t* rch = reinterpret_cast<const int16_t*>(&s.ring[ch][0][kHist]);
+      // line info through a buffer resource (SGPR base, 32-bit lane offset) and
+      // the lane's first line recomputed here: nothing of this rare path stays
+      // live (in VGPRs) across the granule loop
+      const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<uint32_t*>(&g_fast.linfo[combo][0]), (short)0, 576 * 4, 0x00020000);
+      const int L0 = 18 * (lane_fresh() & 31);
 #pragma unroll
       for (int j = 0; j < 18; j++) {
-        const int L = 18 * k + j;
-        const uint32_t inf = li[j];
+        const int L = L0 + j;
+        const uint32_t inf = __builtin_amdgcn_raw_buffer_load_b32(rl, 4 * L, 0, 0);
         const int sfl = inf & 31, sfs = (inf >> 5) & 15, wsrc = (inf >> 9) & 3, wown = (inf >> 11) & 3;
         const int srcr = inf >> 13;
         const bool longlike = !shortblk || (mixed && L < 36);
@@ -410,9 +454,11 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
         const int win = seli(reord, wsrc, wown);
         const int eidx = seli(longlike, 22 * ch + sfl, 44 + 39 * ch + 3 * sfs + win);
         const bool process = longlike ? (shortblk || L < count1) : started;
-        const int xi = s.a.raw[ch][src];
+        const int sk = (src * 3641) >> 16;  // src / 18 for src < 576
+        const int xi = rch[2 * kSlots * sk + (src - 18 * sk)];
         x[j] = self(process, requant_fast(xi, s.expo[eidx]), (float)xi);
       }
+      wave_sync();  // staged lines read before the slots are reused
     }
     stamp(1);
     // ---- MS / intensity stereo with the partner channel's lane (frame.go:304-420) ----
@@ -447,30 +493,37 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
         }
       } else if (!is) {  // MS with short blocks: the reorder can move values past count1
         const float sg = ch ? -1.0f : 1.0f;
+        const int left = msmax - 18 * (lane_fresh() & 31);  // lines of this subband below msmax
 #pragma unroll
         for (int j = 0; j < 18; j++) {
           const float o = xl::xor32(x[j]);
           const float m = (o + sg * x[j]) * inv_sqrt2;
-          x[j] = 18 * k + j < msmax ? m : x[j];
+          x[j] = j < left ? m : x[j];
         }
       } else {
         // MS + intensity stereo: rare, branchy and register hungry, so it runs
         // line-parallel out of LDS -- the ring slots of the current granule are
         // free until the matrixing and hold exactly 2 x 576 floats.
-        float* X0 = &s.ring[0][kHist][0];
-        float* X1 = &s.ring[1][kHist][0];
+        // line L = 18 sb + j of channel c at ring[c][sb][kHist + j]
+        auto at = [&](int c, int L) -> float& {
+          const int sb = (L * 3641) >> 16;  // L / 18
+          return s.ring[c][sb][kHist + L - 18 * sb];
+        };
 #pragma unroll
-        for (int j = 0; j < 18; j++) (ch ? X1 : X0)[18 * k + j] = x[j];
+        for (int j = 0; j < 18; j++) s.ring[ch][k][kHist + j] = x[j];
         wave_sync();
 #pragma unroll 1
         for (int L = lane; L < 576; L += kLanes) {
-          float l = X0[L], r = X1[L];
+          float l = at(0, L), r = at(1, L);
           if (ms && L < msmax) {
             const float nl = (l + r) * inv_sqrt2, nr = (l - r) * inv_sqrt2;
             l = nl;
             r = nr;
           }
-          const uint32_t info = g_fast.linfo[combo][L];
+          const uint32_t info = __builtin_amdgcn_raw_buffer_load_b32(
+              __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(&g_fast.linfo[combo][0]), (short)0, 576 * 4,
+                                                0x00020000),
+              4 * L, 0, 0);
           const int sfl = info & 31, sfs = (info >> 5) & 15, wown = (info >> 11) & 3;
           const bool lp = (!short0 ? (sfl < 21) : (mixed0 && sfl < 8)) && sfl >= nl_is;
           if (lp) {
@@ -488,12 +541,12 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
               r = r * sh.isr[pos][1];
             }
           }
-          X0[L] = l;
-          X1[L] = r;
+          at(0, L) = l;
+          at(1, L) = r;
         }
         wave_sync();
 #pragma unroll
-        for (int j = 0; j < 18; j++) x[j] = (ch ? X1 : X0)[18 * k + j];
+        for (int j = 0; j < 18; j++) x[j] = s.ring[ch][k][kHist + j];
         wave_sync();
       }
     }
@@ -563,7 +616,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
         // packed, pair k = (X[2k], X[17-2k]) holds X[9+q] and X[8-q] of one q
         f2 P[9];
         dct4::dct4_18_pk(x, P);
-        const float4* Wq = sh.winp[bt][k & 1];
+        const float4* Wq = sh.winp[bt][lane_fresh() & 1];
 #pragma unroll
         for (int kk = 0; kk < 9; kk++) {
           const int q = kk <= 4 ? 8 - 2 * kk : 2 * kk - 9;
@@ -580,29 +633,17 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
         }
       }
     }
-    wave_sync();  // raw[] fully consumed before eo[] (same LDS) is written
     stamp(3);
     // prefetch the next granule: lands during the matrixing and window phases
-    // (issued here, not at the top, so its 16 VGPRs are not live across the
-    // front end and IMDCT)
+    // (issued here, not at the top, so its 13 VGPRs are not live across the
+    // front end and IMDCT); buffer resources with SGPR bases and 32-bit lane
+    // offsets: no 64-bit pointer is kept (and spilled) in VGPRs -- a spill
+    // reload costs an s_waitcnt vmcnt(0), which would also wait for this
+    // prefetch
     const bool more = g + 1 < end;
-    uint4 p0 = {0, 0, 0, 0}, p1 = p0, p2 = p0, pd = p0;
+    uint4 pd = {0, 0, 0, 0};
     if (more) {
-      // the next granule through per-granule buffer resources (SGPR bases,
-      // 32-bit lane offsets): no 64-bit pointer is kept (and spilled) in VGPRs
-      // -- a spill reload costs an s_waitcnt vmcnt(0), which would also wait
-      // for this prefetch
-      const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
-          const_cast<int16_t*>(coef + (size_t)(g + 1) * MP3G_COEF_PER_GRANULE), (short)0,
-          (int)(MP3G_COEF_PER_GRANULE * sizeof(int16_t)), 0x00020000);
-      const auto q0 = __builtin_amdgcn_raw_buffer_load_b128(rc, lane * 16, 0, 0);
-      const auto q1 = __builtin_amdgcn_raw_buffer_load_b128(rc, lane * 16 + 1024, 0, 0);
-      p0 = make_uint4(q0[0], q0[1], q0[2], q0[3]);
-      p1 = make_uint4(q1[0], q1[1], q1[2], q1[3]);
-      if (lane < 16) {
-        const auto q2 = __builtin_amdgcn_raw_buffer_load_b128(rc, lane * 16 + 2048, 0, 0);
-        p2 = make_uint4(q2[0], q2[1], q2[2], q2[3]);
-      }
+      load_lines(coef, g + 1, lane, cw);
       if (lane < 10) {
         const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<mp3g_granule*>(gran + g + 1), (short)0, (int)sizeof(mp3g_granule), 0x00020000);
@@ -616,28 +657,22 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     //      the 32 distinct values X of V = synthNWin * S with an in-lane fast
     //      DCT-II-32 on float pairs (dct32.h), in place ----
     if (need_v && act) {
-      float* Sc = &s.ring[ch][kHist][k];
 #pragma unroll
-      for (int j = 0; j < 18; j++) Sc[kRow * j] = o[j];
+      for (int j = 0; j < 18; j++) s.ring[ch][k][kHist + j] = o[j];
     }
     wave_sync();
     stamp(4);
     {
       const int slot = lane & 31;  // lane = (ch, slot), slots 0..17
       if (need_v && act && slot < 18) {
-        float* row = &s.ring[ch][kHist + slot][0];
-        dct32::f2 sp[16], xp[16];
-        const float4* r4 = reinterpret_cast<const float4*>(row);
+        float* colu = &s.ring[ch][0][kHist + slot];  // S[k] / X at colu[kSlots * k]
+        dct32::f2 sp[16];
 #pragma unroll
-        for (int q = 0; q < 8; q++) {
-          const float4 v = r4[q];
-          sp[2 * q] = (dct32::f2){v.x, v.y};
-          sp[2 * q + 1] = (dct32::f2){v.z, v.w};
-        }
-        dct32::dct2_32(sp, xp);
-        dct32::f2* w2 = reinterpret_cast<dct32::f2*>(row);
-#pragma unroll
-        for (int t = 0; t < 16; t++) w2[t] = xp[t];
+        for (int q = 0; q < 16; q++) sp[q] = (dct32::f2){colu[kSlots * 2 * q], colu[kSlots * (2 * q + 1)]};
+        dct32::dct2_32_to(sp, [&](int t, dct32::f2 v) {
+          colu[kSlots * 2 * t] = v.x;
+          colu[kSlots * (2 * t + 1)] = v.y;
+        });
       }
     }
     stamp(5);
@@ -648,13 +683,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     //      before the PCM stores are issued -- vmcnt counts loads and stores in
     //      issue order, so a wait for the prefetch after the stores would wait
     //      for the stores too ----
-    if (more) {
-      uint4* dst = reinterpret_cast<uint4*>(&s.a.raw[0][0]);
-      dst[lane] = p0;
-      dst[lane + 64] = p1;
-      if (lane < 16) dst[lane + 128] = p2;
-      if (lane < 10) reinterpret_cast<uint4*>(&s.desc)[lane] = pd;
-    }
+    if (more && lane < 10) reinterpret_cast<uint4*>(&s.desc)[lane] = pd;
 
     // ---- 16-tap window over the X ring -> s16 PCM, stored straight to HBM ----
     // (lanes of an absent channel compute values that are never stored)
@@ -676,14 +705,15 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       // v = 2p - 2t: every operand pair is two rows of one column, i.e. one
       // ds_read2_b32 that lands as the packed operand, and each feeds up to 8
       // accumulator pairs.
-      const float* R = &s.ring[ch][0][0];
+      const f2* RA = reinterpret_cast<const f2*>(&s.ring[ch][pa][0]);
+      const float* RB = &s.ring[ch][pb][0];
       f2 acc2[9];
 #pragma unroll
       for (int p = 0; p < 9; p++) acc2[p] = bcast(0.0f);
 #pragma unroll
       for (int v = -14; v <= 16; v += 2) {
-        const f2 A = {R[(kHist + v) * kRow + pa], R[(kHist + v + 1) * kRow + pa]};
-        const f2 B = {R[(kHist + v - 1) * kRow + pb], R[(kHist + v) * kRow + pb]};
+        const f2 A = RA[(kHist + v) / 2];  // slots (16+v, 17+v): 8-B aligned
+        const f2 B = {RB[kHist + v - 1], RB[kHist + v]};
 #pragma unroll
         for (int t = 0; t < 8; t++) {
           const int p = v / 2 + t;
@@ -710,10 +740,12 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     wave_sync();  // ring reads done
     stamp(6);
 
-    // ---- history shift (channels this granule touched) ----
-    for (int e = lane; e < nch * (kHist * kRow / 4); e += kLanes) {
-      const int c = e / (kHist * kRow / 4), r4 = e % (kHist * kRow / 4);
-      reinterpret_cast<float4*>(&s.ring[c][0][0])[r4] = reinterpret_cast<const float4*>(&s.ring[c][18][0])[r4];
+    // ---- history shift (channels this granule touched): lane = (c, column),
+    //      slots 18..33 -> 0..15 as 8-B moves ----
+    if (ch < nch) {
+      f2* col = reinterpret_cast<f2*>(&s.ring[ch][k][0]);
+#pragma unroll
+      for (int q = 0; q < 8; q++) col[q] = col[9 + q];
     }
     wave_sync();
     stamp(7);
@@ -730,7 +762,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     }
     for (int e = lane; e < 2 * 1024; e += kLanes) {
       const int c = e >> 10, blk = (e >> 6) & 15, i = e & 63;
-      so->vvec[c][64 * blk + i] = blk < kHist ? v_from_x(s.ring[c][kHist - 1 - blk], i) : 0.0f;
+      so->vvec[c][64 * blk + i] = blk < 15 ? v_from_x(&s.ring[c][0][kHist - 1 - blk], i) : 0.0f;
     }
   }
   if constexpr (kStamp) {
