@@ -18,8 +18,8 @@
 // v_pk_* instructions.  Reassociated like the rest of the fast mode (+-1 LSB
 // of PCM; tests/test_dct32.py checks it against float64).
 //
-// Output order: X leaves as 16 pairs (kPairM[t][0], kPairM[t][1]); the ring
-// row of a slot stores pair t at positions 2t, 2t + 1 (kPosOfM = inverse).
+// Output order: X leaves as 16 pairs (kPairM[t][0], kPairM[t][1]); the fast
+// kernel stores pair t in ring columns kColX[t], kColY[t] (kPosOfM: X[m]'s column).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -43,9 +43,16 @@ using pk::swp;
 // m of the two values of output pair t
 constexpr int kPairM[16][2] = {{1, 31},  {5, 27},  {9, 23},  {13, 19}, {17, 15}, {21, 11}, {25, 7},  {29, 3},
                                {2, 30},  {10, 22}, {18, 14}, {26, 6},  {4, 12},  {20, 28}, {0, 16},  {8, 24}};
-// ring-row position of X[m]
-constexpr int kPosOfM[32] = {28, 0,  16, 15, 24, 2,  23, 13, 30, 4,  18, 11, 25, 6,  21, 9,
-                             29, 8,  20, 7,  26, 10, 19, 5,  31, 12, 22, 3,  27, 14, 17, 1};
+// Positions in the fast kernel's ring column set (32 columns, 34 dwords
+// apart, granule_fast.hip): pair t goes to columns (kColX[t], kColY[t]), so
+// X[m] sits in column kPosOfM[m].  The window's odd taps read X[0..16] in one
+// column each; 34c mod 32 = 2c mod 32 puts columns c and c + 16 in one bank,
+// and this assignment gives those 17 values 16 distinct banks (one pair
+// shares: 17 > 16).
+constexpr int kColX[16] = {18, 4, 21, 6, 22, 9, 24, 11, 27, 12, 28, 15, 0, 16, 2, 31};
+constexpr int kColY[16] = {19, 5, 20, 7, 23, 8, 25, 10, 26, 13, 29, 14, 1, 17, 3, 30};
+constexpr int kPosOfM[32] = {2,  18, 27, 10, 0,  4,  14, 25, 31, 21, 12, 8,  1, 6,  29, 23,
+                             3,  22, 28, 7,  16, 9,  13, 20, 30, 24, 15, 5,  17, 11, 26, 19};
 
 // Twiddles, float literals: e^{-i pi (4n+1)/64} (pre, DCT4_16), e^{-i pi k/16}
 // (post, DCT4_16), e^{-i pi (4n+1)/32} and e^{-i pi k/8} (DCT4_8): (cos, sin).

@@ -263,7 +263,8 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       const float sq = par && (q & 1) ? -1.0f : 1.0f, sr = par && !(q & 1) ? -1.0f : 1.0f;  // j = q, 17 - q
       sh.winp[bt][par][q] = make_float4(W[q] * sq, -W[17 - q] * sr, -W[18 + q] * sq, -W[35 - q] * sr);
     }
-    for (int e = t; e < 16; e += kLanes * kWaves) (&sh.isr[0][0])[e] = (&g_fast.is_ratio[0][0])[e];
+    // is_pos 0..6 -> isRatios (frame.go:304-306); 7 -> (1, 1): no change
+    for (int e = t; e < 16; e += kLanes * kWaves) (&sh.isr[0][0])[e] = e < 14 ? (&g_fast.is_ratio[0][0])[e] : 1.0f;
     for (int e = t; e < 32 * 16; e += kLanes * kWaves) (&sh.dwin[0][0])[e] = (&g_fast.dwin[0][0])[e] * 32767.0f;
     for (int e = t; e < kCombos * 32; e += kLanes * kWaves) (&sh.lband[0][0])[e] = (&g_fast.lband[0][0])[e];
   }
@@ -350,6 +351,15 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
   // takes a higher priority, which keeps the co-resident waves abreast.
   const uint32_t span = end - w;
   for (uint32_t g = w; g < end; g++) {
+#ifdef MP3G_EXP_SALU
+    // timing experiment only (tools/build_variant.sh): extra scalar ALU work
+    {
+      uint32_t d = g;
+#pragma unroll
+      for (int i = 0; i < MP3G_EXP_SALU; i++) asm volatile("s_add_u32 %0, %0, 1" : "+s"(d));
+    }
+#endif
+#ifndef MP3G_EXP_NOPRIO
     {
       const uint32_t q = (4u * (end - g) - 1u) / span;  // 3 (most left) .. 0
       if (q >= 3) __builtin_amdgcn_s_setprio(3);
@@ -357,6 +367,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       else if (q == 1) __builtin_amdgcn_s_setprio(1);
       else __builtin_amdgcn_s_setprio(0);
     }
+#endif
     const bool out = g >= out_first;
     // does a replayed granule's V feed anything? (see v2 / DESIGN.md halo)
     bool need_v = true;
@@ -466,7 +477,11 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       const mp3g_channel& C0 = s.desc.ch[0];
       const int c1r = s.desc.ch[1].count1;
       const int msmax = max((int)C0.count1, c1r);
+#ifdef MP3G_EXP_NOIS
+      const bool ms = h & 0x20u, is = false;  // timing experiment only: wrong PCM
+#else
       const bool ms = h & 0x20u, is = h & 0x10u;
+#endif
       const bool short0 = C0.win_switch_flag == 1 && C0.block_type == 2;
       const bool mixed0 = C0.mixed_block_flag != 0;
       int nl_is = 0, ns_is = 0;  // first long / short band starting at or above channel 1's count1
@@ -475,79 +490,59 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
 #pragma unroll
       for (int b = 0; b < 14; b++) ns_is += 3 * (int)g_fast.sfb_short[combo][b] < c1r;
       const float inv_sqrt2 = 0.70710678118654752440f;
-      if (!is && all_long) {
-        // MS only on long blocks (the common joint-stereo case): lines at or
-        // above max(count1) are 0 in both channels, where (l +- r)c is 0 too,
-        // so every line is transformed.  Two lines per step: one swap gives
-        // lanes < 32 (l, r) of line j and lanes >= 32 those of line j + 1,
-        // (l + r)c, (l - r)c in one packed pair, a second swap hands back
-        // L' / R' of both lines to their channels' lanes.
+      if (ms) {
+        // MS: L' = (l + r)c, R' = (l - r)c for lines below max(count1)
+        // (frame.go:362-377).  Two lines per step: one swap gives lanes < 32
+        // (l, r) of line j and lanes >= 32 those of line j + 1, (l + r)c,
+        // (l - r)c in one packed pair, a second swap hands back L' / R' of
+        // both lines to their channels' lanes.  Long blocks without intensity
+        // stereo transform every line: at or above max(count1) both channels
+        // are 0, where (l +- r)c is 0 too.  Otherwise lines >= max(count1) keep
+        // their values (the reorder can move values past count1; IS follows).
+        const bool keep_tail = !(all_long && !is);  // wave-uniform
+        const int left = msmax - 18 * (lane_fresh() & 31);  // lines of this subband below msmax
 #pragma unroll
         for (int j = 0; j < 18; j += 2) {
           const auto r = __builtin_amdgcn_permlane32_swap(__float_as_int(x[j]), __float_as_int(x[j + 1]), false, false);
           const float a = __int_as_float(r[0]), b = __int_as_float(r[1]);
           const f2 pq = (f2){a + b, a - b} * bcast(inv_sqrt2);
           const auto r2 = __builtin_amdgcn_permlane32_swap(__float_as_int(pq.x), __float_as_int(pq.y), false, false);
-          x[j] = __int_as_float(r2[0]);
-          x[j + 1] = __int_as_float(r2[1]);
+          const float n0 = __int_as_float(r2[0]), n1 = __int_as_float(r2[1]);
+          x[j] = keep_tail ? (j < left ? n0 : x[j]) : n0;
+          x[j + 1] = keep_tail ? (j + 1 < left ? n1 : x[j + 1]) : n1;
         }
-      } else if (!is) {  // MS with short blocks: the reorder can move values past count1
-        const float sg = ch ? -1.0f : 1.0f;
-        const int left = msmax - 18 * (lane_fresh() & 31);  // lines of this subband below msmax
+      }
+      if (is) {
+        // Intensity stereo per line of this lane (frame.go:308-359, :379-419):
+        // bands at or above channel 1's count1, ratio index from CHANNEL 0's
+        // scale factors, each channel scaled by its own ratio (is_pos 7 = no
+        // change: isr[7] = (1, 1)).  Long blocks: the line's band from the
+        // subband's band-start mask (as in the requantization); short / mixed
+        // blocks: the line info table.
+        const int k0 = lane_fresh() & 31;
+        if (!short0) {
+          const uint32_t lb = sh.lband[combo][k0];
 #pragma unroll
-        for (int j = 0; j < 18; j++) {
-          const float o = xl::xor32(x[j]);
-          const float m = (o + sg * x[j]) * inv_sqrt2;
-          x[j] = j < left ? m : x[j];
+          for (int j = 0; j < 18; j++) {
+            const int sfl = (int)(lb & 31u) + __builtin_popcount((lb >> 5) & ((2u << j) - 1u));
+            const int pos = min((int)C0.scalefac_l[min(sfl, 21)], 7);
+            const float rr = sh.isr[pos][ch];
+            x[j] = (sfl < 21 && sfl >= nl_is) ? x[j] * rr : x[j];
+          }
+        } else {
+          const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
+              const_cast<uint32_t*>(&g_fast.linfo[combo][0]), (short)0, 576 * 4, 0x00020000);
+#pragma unroll
+          for (int j = 0; j < 18; j++) {
+            const uint32_t info = __builtin_amdgcn_raw_buffer_load_b32(rl, 4 * (18 * k0 + j), 0, 0);
+            const int sfl = info & 31, sfs = (info >> 5) & 15, wown = (info >> 11) & 3;
+            const bool lp = mixed0 && sfl < 8 && sfl >= nl_is;
+            const bool sp = sfs < 12 && (!mixed0 || sfs >= 3) && sfs >= ns_is;
+            const int pl = lp ? min((int)C0.scalefac_l[min(sfl, 21)], 7) : 7;
+            const int ps = sp ? min((int)C0.scalefac_s[min(sfs, 12)][min(wown, 2)], 7) : 7;
+            x[j] = x[j] * sh.isr[pl][ch] * sh.isr[ps][ch];
+          }
         }
-      } else {
-        // MS + intensity stereo: rare, branchy and register hungry, so it runs
-        // line-parallel out of LDS -- the ring slots of the current granule are
-        // free until the matrixing and hold exactly 2 x 576 floats.
-        // line L = 18 sb + j of channel c at ring[c][sb][kHist + j]
-        auto at = [&](int c, int L) -> float& {
-          const int sb = (L * 3641) >> 16;  // L / 18
-          return s.ring[c][sb][kHist + L - 18 * sb];
-        };
-#pragma unroll
-        for (int j = 0; j < 18; j++) s.ring[ch][k][kHist + j] = x[j];
-        wave_sync();
-#pragma unroll 1
-        for (int L = lane; L < 576; L += kLanes) {
-          float l = at(0, L), r = at(1, L);
-          if (ms && L < msmax) {
-            const float nl = (l + r) * inv_sqrt2, nr = (l - r) * inv_sqrt2;
-            l = nl;
-            r = nr;
-          }
-          const uint32_t info = __builtin_amdgcn_raw_buffer_load_b32(
-              __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(&g_fast.linfo[combo][0]), (short)0, 576 * 4,
-                                                0x00020000),
-              4 * L, 0, 0);
-          const int sfl = info & 31, sfs = (info >> 5) & 15, wown = (info >> 11) & 3;
-          const bool lp = (!short0 ? (sfl < 21) : (mixed0 && sfl < 8)) && sfl >= nl_is;
-          if (lp) {
-            const int pos = C0.scalefac_l[sfl];
-            if (pos < 7) {
-              l = l * sh.isr[pos][0];
-              r = r * sh.isr[pos][1];
-            }
-          }
-          const bool sp = short0 && sfs < 12 && (!mixed0 || sfs >= 3) && sfs >= ns_is;
-          if (sp) {
-            const int pos = C0.scalefac_s[sfs][wown];
-            if (pos < 7) {
-              l = l * sh.isr[pos][0];
-              r = r * sh.isr[pos][1];
-            }
-          }
-          at(0, L) = l;
-          at(1, L) = r;
-        }
-        wave_sync();
-#pragma unroll
-        for (int j = 0; j < 18; j++) x[j] = s.ring[ch][k][kHist + j];
-        wave_sync();
       }
     }
     {
@@ -670,8 +665,8 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
 #pragma unroll
         for (int q = 0; q < 16; q++) sp[q] = (dct32::f2){colu[kSlots * 2 * q], colu[kSlots * (2 * q + 1)]};
         dct32::dct2_32_to(sp, [&](int t, dct32::f2 v) {
-          colu[kSlots * 2 * t] = v.x;
-          colu[kSlots * (2 * t + 1)] = v.y;
+          colu[kSlots * dct32::kColX[t]] = v.x;
+          colu[kSlots * dct32::kColY[t]] = v.y;
         });
       }
     }

@@ -19,8 +19,12 @@ extern "C" void dct32_host(const float* S, float* X, int n) {
   }
 }
 
-extern "C" void dct32_tables(int* pair_m, int* pos_of_m) {
-  for (int t = 0; t < 32; t++) pair_m[t] = mp3g::dct32::kPairM[t / 2][t % 2];
+// col_m[c] = the m stored in ring column c (from kPairM, kColX, kColY)
+extern "C" void dct32_tables(int* col_m, int* pos_of_m) {
+  for (int t = 0; t < 16; t++) {
+    col_m[mp3g::dct32::kColX[t]] = mp3g::dct32::kPairM[t][0];
+    col_m[mp3g::dct32::kColY[t]] = mp3g::dct32::kPairM[t][1];
+  }
   for (int m = 0; m < 32; m++) pos_of_m[m] = mp3g::dct32::kPosOfM[m];
 }
 

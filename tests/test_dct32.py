@@ -38,11 +38,13 @@ def ref64(S):
 
 
 def test_tables_are_a_permutation(lib):
-    pm = np.zeros(32, np.int32)
+    col_m = np.full(32, -1, np.int32)
     pos = np.zeros(32, np.int32)
-    lib.dct32_tables(pm.ctypes.data, pos.ctypes.data)
-    assert sorted(pm) == list(range(32))
-    assert all(pm[pos[m]] == m for m in range(32))
+    lib.dct32_tables(col_m.ctypes.data, pos.ctypes.data)
+    assert sorted(col_m) == list(range(32))
+    assert all(col_m[pos[m]] == m for m in range(32))
+    # the window's odd-tap values X[0..16]: 16 distinct banks of 34-dword columns
+    assert len({(34 * int(pos[m])) % 32 for m in range(17)}) == 16
 
 
 @pytest.mark.parametrize("scale", [1e-6, 1.0, 3e3])
