@@ -287,7 +287,11 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
   // loop state as wave-uniform 32-bit scalars (plans are limited to < 2^32
   // granules): keeps it in SGPRs, so per-granule header reads are scalar loads
   // (lgkmcnt) that never wait behind the prefetch loads or PCM stores (vmcnt)
+#ifdef MP3G_EXP_NOHALO
+  const uint32_t w = __builtin_amdgcn_readfirstlane((uint32_t)cd.out_first);  // timing experiment only: wrong PCM
+#else
   const uint32_t w = __builtin_amdgcn_readfirstlane((uint32_t)w64);
+#endif
   const uint32_t out_first = __builtin_amdgcn_readfirstlane((uint32_t)cd.out_first);
   const uint32_t end = __builtin_amdgcn_readfirstlane((uint32_t)(cd.out_first + cd.n_out));
   const mp3g_state* sin = state_in ? state_in + cd.stream : nullptr;
