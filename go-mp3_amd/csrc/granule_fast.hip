@@ -101,8 +101,9 @@ struct __align__(16) WaveSmem {
   // turns them into X in place; before that they stage the raw coefficients
   // of short-block granules (reorder gather) and the intensity-stereo pass
   float ring[2][32][kSlots];
-  // requantization exponents n4 of the long bands [ch][sfb] and short bands [ch][sfb][win]
-  int16_t expo[2 * 22 + 2 * 39];
+  // requantization exponents n4 / 4 (float16, exact) of the long bands
+  // [ch][sfb] and short bands [ch][sfb][win]
+  _Float16 expo[2 * 22 + 2 * 39];
   mp3g_granule desc;
 };
 
@@ -198,10 +199,14 @@ __device__ __forceinline__ int seli(bool c, int a, int b) {
 // sign(x) |x|^(4/3) 2^(n4/4) = ldexp(2^(4/3 log2|x| + (n4 & 3)/4), n4 >> 2), signed:
 // two transcendental VALU ops instead of the float64 table gather of the
 // reference (frame.go:148-155); relative error ~1e-6 (x = 0 -> exactly 0).
-__device__ __forceinline__ float requant_fast(int xi, int n4) {
+// The band exponent arrives as e = n4 / 4 in float16 (exact: n4 is an integer
+// in [-390, 45], so e needs 11 significant bits), and the whole power goes
+// through one exp2: 2^(4/3 log2|x| + e).  For the values that reach the PCM
+// (|e| and |t| below ~32) the input rounding of t adds <= 2^-19 relative error.
+__device__ __forceinline__ float requant_fast(int xi, _Float16 e) {
   const float xf = (float)xi;
-  const float t = __builtin_amdgcn_logf(fabsf(xf)) * (4.0f / 3.0f) + 0.25f * (float)(n4 & 3);
-  return copysignf(ldexpf(__builtin_amdgcn_exp2f(t), n4 >> 2), xf);
+  const float t = __builtin_fmaf(__builtin_amdgcn_logf(fabsf(xf)), 4.0f / 3.0f, (float)e);
+  return copysignf(__builtin_amdgcn_exp2f(t), xf);
 }
 
 // The lane id, recomputed where it is used (asm volatile: not hoisted out of
@@ -407,7 +412,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
         v = (int)D.global_gain - 210 - 8 * (int)D.subblock_gain[win] -
             (D.scalefac_scale ? 4 : 2) * (int)D.scalefac_s[sfb][win];
       }
-      s.expo[e] = v;
+      s.expo[e] = (_Float16)(0.25f * (float)v);
     }
     const int count1 = C.count1;
     const bool shortblk = C.win_switch_flag == 1 && C.block_type == 2;
@@ -430,7 +435,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       }
       // long band of line j: first band of the subband + band starts among lines 1..j
       const uint32_t lb = sh.lband[combo][k];
-      int ex[18];
+      _Float16 ex[18];
 #pragma unroll
       for (int j = 0; j < 18; j++)
         ex[j] = s.expo[22 * ch + (int)(lb & 31u) + __builtin_popcount((lb >> 5) & ((2u << j) - 1u))];
