@@ -417,9 +417,6 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     const int count1 = C.count1;
     const bool shortblk = C.win_switch_flag == 1 && C.block_type == 2;
     const bool mixed = C.mixed_block_flag != 0;
-    int nsfs = 0;  // short bands whose first line lies below count1 (frame.go:229-255 loop bound)
-#pragma unroll
-    for (int b = 0; b < 13; b++) nsfs += 3 * (int)g_fast.sfb_short[combo][b] < count1;
     wave_sync();
     stamp(0);
 
@@ -446,6 +443,9 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
 #pragma unroll
       for (int j = 0; j < 18; j++) x[j] = requant_fast(xi[j], ex[j]);
     } else {
+      int nsfs = 0;  // short bands whose first line lies below count1 (frame.go:229-255 loop bound)
+#pragma unroll
+      for (int b = 0; b < 13; b++) nsfs += 3 * (int)g_fast.sfb_short[combo][b] < count1;
       // reorder gather: the channel's raw lines staged in the current slots of
       // the ring, lane (ch, sb) writing its 9 dwords to column sb
       {
@@ -484,8 +484,9 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     // ---- MS / intensity stereo with the partner channel's lane (frame.go:304-420) ----
     if (nch == 2 && hdr_mode(h) == 1 && (h & 0x30u)) {
       const mp3g_channel& C0 = s.desc.ch[0];
-      const int c1r = s.desc.ch[1].count1;
-      const int msmax = max((int)C0.count1, c1r);
+      // wave-uniform (SGPRs): the comparisons below stay scalar
+      const int c1r = __builtin_amdgcn_readfirstlane((int)s.desc.ch[1].count1);
+      const int msmax = max(__builtin_amdgcn_readfirstlane((int)C0.count1), c1r);
 #ifdef MP3G_EXP_NOIS
       const bool ms = h & 0x20u, is = false;  // timing experiment only: wrong PCM
 #else
@@ -493,11 +494,6 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
 #endif
       const bool short0 = C0.win_switch_flag == 1 && C0.block_type == 2;
       const bool mixed0 = C0.mixed_block_flag != 0;
-      int nl_is = 0, ns_is = 0;  // first long / short band starting at or above channel 1's count1
-#pragma unroll
-      for (int b = 0; b < 23; b++) nl_is += (int)g_fast.sfb_long[combo][b] < c1r;
-#pragma unroll
-      for (int b = 0; b < 14; b++) ns_is += 3 * (int)g_fast.sfb_short[combo][b] < c1r;
       const float inv_sqrt2 = 0.70710678118654752440f;
       if (ms) {
         // MS: L' = (l + r)c, R' = (l - r)c for lines below max(count1)
@@ -508,17 +504,26 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
         // stereo transform every line: at or above max(count1) both channels
         // are 0, where (l +- r)c is 0 too.  Otherwise lines >= max(count1) keep
         // their values (the reorder can move values past count1; IS follows).
-        const bool keep_tail = !(all_long && !is);  // wave-uniform
-        const int left = msmax - 18 * (lane_fresh() & 31);  // lines of this subband below msmax
-#pragma unroll
-        for (int j = 0; j < 18; j += 2) {
-          const auto r = __builtin_amdgcn_permlane32_swap(__float_as_int(x[j]), __float_as_int(x[j + 1]), false, false);
+        auto ms_pair = [&](float& u, float& v) {
+          const auto r = __builtin_amdgcn_permlane32_swap(__float_as_int(u), __float_as_int(v), false, false);
           const float a = __int_as_float(r[0]), b = __int_as_float(r[1]);
           const f2 pq = (f2){a + b, a - b} * bcast(inv_sqrt2);
           const auto r2 = __builtin_amdgcn_permlane32_swap(__float_as_int(pq.x), __float_as_int(pq.y), false, false);
-          const float n0 = __int_as_float(r2[0]), n1 = __int_as_float(r2[1]);
-          x[j] = keep_tail ? (j < left ? n0 : x[j]) : n0;
-          x[j + 1] = keep_tail ? (j + 1 < left ? n1 : x[j + 1]) : n1;
+          u = __int_as_float(r2[0]);
+          v = __int_as_float(r2[1]);
+        };
+        if (all_long && !is) {  // wave-uniform
+#pragma unroll
+          for (int j = 0; j < 18; j += 2) ms_pair(x[j], x[j + 1]);
+        } else {
+          const int left = msmax - 18 * (lane_fresh() & 31);  // lines of this subband below msmax
+#pragma unroll
+          for (int j = 0; j < 18; j += 2) {
+            float n0 = x[j], n1 = x[j + 1];
+            ms_pair(n0, n1);
+            x[j] = j < left ? n0 : x[j];
+            x[j + 1] = j + 1 < left ? n1 : x[j + 1];
+          }
         }
       }
       if (is) {
@@ -529,6 +534,11 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
         // subband's band-start mask (as in the requantization); short / mixed
         // blocks: the line info table.
         const int k0 = lane_fresh() & 31;
+        int nl_is = 0, ns_is = 0;  // first long / short band starting at or above channel 1's count1
+#pragma unroll
+        for (int b = 0; b < 23; b++) nl_is += (int)g_fast.sfb_long[combo][b] < c1r;
+#pragma unroll
+        for (int b = 0; b < 14; b++) ns_is += 3 * (int)g_fast.sfb_short[combo][b] < c1r;
         if (!short0) {
           const uint32_t lb = sh.lband[combo][k0];
 #pragma unroll
@@ -673,6 +683,15 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
         dct32::f2 sp[16];
 #pragma unroll
         for (int q = 0; q < 16; q++) sp[q] = (dct32::f2){colu[kSlots * 2 * q], colu[kSlots * (2 * q + 1)]};
+#ifdef MP3G_EXP_NODCT
+        // timing experiment only: X = S (wrong PCM)
+#pragma unroll
+        for (int t = 0; t < 16; t++) {
+          colu[kSlots * dct32::kColX[t]] = sp[t].x;
+          colu[kSlots * dct32::kColY[t]] = sp[t].y;
+        }
+        if (false)
+#endif
         dct32::dct2_32_to(sp, [&](int t, dct32::f2 v) {
           colu[kSlots * dct32::kColX[t]] = v.x;
           colu[kSlots * dct32::kColY[t]] = v.y;
@@ -721,6 +740,9 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
 #pragma unroll
         for (int t = 0; t < 8; t++) {
           const int p = v / 2 + t;
+#ifdef MP3G_EXP_HALFWIN
+          if (t & 1) continue;  // timing experiment only: half the taps (wrong PCM)
+#endif
           if (p >= 0 && p < 9) {
             acc2[p] = pfma(bcast(dw[2 * t]), A, acc2[p]);
             acc2[p] = pfma(bcast(dw[2 * t + 1]), B, acc2[p]);
