@@ -101,10 +101,10 @@ struct __align__(16) WaveSmem {
   // turns them into X in place; before that they stage the raw coefficients
   // of short-block granules (reorder gather) and the intensity-stereo pass
   float ring[2][32][kSlots];
+  mp3g_granule desc;  // 16-B aligned: the channels' first 8 bytes are one 8-B read each
   // requantization exponents n4 / 4 (float16, exact) of the long bands
   // [ch][sfb] and short bands [ch][sfb][win]
   _Float16 expo[2 * 22 + 2 * 39];
-  mp3g_granule desc;
 };
 
 // Raw coefficients of lane (ch, sb) of granule g: its 18 lines, 36 B at
@@ -358,7 +358,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
   // youngest finishes last, alone and latency-bound (c2 timeline: loop spans
   // 34 .. 101 us for identical chunks).  A wave with more of its chunk left
   // takes a higher priority, which keeps the co-resident waves abreast.
-  const uint32_t span = end - w;
+  const uint32_t span = end - w, span2 = 2 * span, span3 = 3 * span;
   for (uint32_t g = w; g < end; g++) {
 #ifdef MP3G_EXP_SALU
     // timing experiment only (tools/build_variant.sh): extra scalar ALU work
@@ -370,10 +370,10 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
 #endif
 #ifndef MP3G_EXP_NOPRIO
     {
-      const uint32_t q = (4u * (end - g) - 1u) / span;  // 3 (most left) .. 0
-      if (q >= 3) __builtin_amdgcn_s_setprio(3);
-      else if (q == 2) __builtin_amdgcn_s_setprio(2);
-      else if (q == 1) __builtin_amdgcn_s_setprio(1);
+      const uint32_t left4 = 4u * (end - g);  // priority floor(4 * left / span), 3 .. 0
+      if (left4 > span3) __builtin_amdgcn_s_setprio(3);
+      else if (left4 > span2) __builtin_amdgcn_s_setprio(2);
+      else if (left4 > span) __builtin_amdgcn_s_setprio(1);
       else __builtin_amdgcn_s_setprio(0);
     }
 #endif
@@ -385,38 +385,50 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     const uint32_t h = __builtin_amdgcn_readfirstlane(s.desc.header);
     const int nch = hdr_nch(h), combo = hdr_combo(h);
     const bool act = ch < nch;
-    // lanes of an absent channel mirror channel 0's block layout (no extra divergence)
-    const mp3g_channel& C = s.desc.ch[act ? ch : 0];
-
-
+    // the channels' scalar parameters in SGPRs (one 8-B LDS read each):
+    // dword 0 = count1 | global_gain << 16 | scalefac_scale << 24,
+    // dword 1 = preflag | win_switch_flag << 8 | block_type << 16 | mixed_block_flag << 24
+    uint32_t cp0[2], cp1[2];
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+      const uint2 v = *reinterpret_cast<const uint2*>(&s.desc.ch[c]);
+      cp0[c] = __builtin_amdgcn_readfirstlane(v.x);
+      cp1[c] = __builtin_amdgcn_readfirstlane(v.y);
+    }
+    auto is_short = [](uint32_t d1) { return (d1 & 0x00ffff00u) == 0x00020100u; };  // win_switch 1, block_type 2
     // wave-uniform: every channel of this granule is a long block (no reorder)
-    const bool all_long = __builtin_amdgcn_readfirstlane(
-        !(s.desc.ch[0].win_switch_flag == 1 && s.desc.ch[0].block_type == 2) &&
-        (nch == 1 || !(s.desc.ch[1].win_switch_flag == 1 && s.desc.ch[1].block_type == 2)));
+    const bool all_long = !is_short(cp1[0]) && (nch == 1 || !is_short(cp1[1]));
+    // this lane's channel (lanes of an absent channel mirror channel 0's block
+    // layout: no extra divergence)
+    const uint32_t d0 = (act && ch) ? cp0[1] : cp0[0], d1 = (act && ch) ? cp1[1] : cp1[0];
 
     // ---- per-granule front-end parameters: band exponents (long bands only
-    //      when no channel has short blocks), band thresholds ----
-    for (int e = lane; e < (all_long ? 2 * 22 : 2 * 22 + 2 * 39); e += kLanes) {
-      int c, v;
+    //      when no channel has short blocks) ----
+    {
+      // long bands: lane = (c, sfb), 44 lanes
+      const int e = lane_fresh();
       if (e < 44) {
-        c = e >= 22;
-        const int sfb = e - 22 * c;
-        const mp3g_channel& D = s.desc.ch[c];
-        v = (int)D.global_gain - 210 -
-            (D.scalefac_scale ? 4 : 2) * ((int)D.scalefac_l[sfb] + (int)D.preflag * kPretab(sfb));
-      } else {
-        const int r0 = e - 44;
-        c = r0 >= 39;
-        const int r = r0 - 39 * c, sfb = r / 3, win = r - 3 * sfb;
-        const mp3g_channel& D = s.desc.ch[c];
-        v = (int)D.global_gain - 210 - 8 * (int)D.subblock_gain[win] -
-            (D.scalefac_scale ? 4 : 2) * (int)D.scalefac_s[sfb][win];
+        const int c = e >= 22, sfb = e - 22 * c;
+        const uint32_t a0 = c ? cp0[1] : cp0[0], a1 = c ? cp1[1] : cp1[0];
+        const int v = (int)((a0 >> 16) & 0xffu) - 210 -
+                      ((a0 >> 24) ? 4 : 2) * ((int)s.desc.ch[c].scalefac_l[sfb] + (int)(a1 & 0xffu) * kPretab(sfb));
+        s.expo[e] = (_Float16)(0.25f * (float)v);
       }
-      s.expo[e] = (_Float16)(0.25f * (float)v);
+      if (!all_long) {
+        // short bands: (c, sfb, win), 78 entries
+        for (int r0 = e; r0 < 2 * 39; r0 += kLanes) {
+          const int c = r0 >= 39, r = r0 - 39 * c, sfb = r / 3, win = r - 3 * sfb;
+          const uint32_t a0 = c ? cp0[1] : cp0[0];
+          const mp3g_channel& D = s.desc.ch[c];
+          const int v = (int)((a0 >> 16) & 0xffu) - 210 - 8 * (int)D.subblock_gain[win] -
+                        ((a0 >> 24) ? 4 : 2) * (int)D.scalefac_s[sfb][win];
+          s.expo[44 + r0] = (_Float16)(0.25f * (float)v);
+        }
+      }
     }
-    const int count1 = C.count1;
-    const bool shortblk = C.win_switch_flag == 1 && C.block_type == 2;
-    const bool mixed = C.mixed_block_flag != 0;
+    const int count1 = (int)(d0 & 0xffffu);
+    const bool shortblk = is_short(d1);
+    const bool mixed = (d1 >> 24) != 0;
     wave_sync();
     stamp(0);
 
@@ -484,16 +496,15 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     // ---- MS / intensity stereo with the partner channel's lane (frame.go:304-420) ----
     if (nch == 2 && hdr_mode(h) == 1 && (h & 0x30u)) {
       const mp3g_channel& C0 = s.desc.ch[0];
-      // wave-uniform (SGPRs): the comparisons below stay scalar
-      const int c1r = __builtin_amdgcn_readfirstlane((int)s.desc.ch[1].count1);
-      const int msmax = max(__builtin_amdgcn_readfirstlane((int)C0.count1), c1r);
+      const int c1r = (int)(cp0[1] & 0xffffu);
+      const int msmax = max((int)(cp0[0] & 0xffffu), c1r);
 #ifdef MP3G_EXP_NOIS
       const bool ms = h & 0x20u, is = false;  // timing experiment only: wrong PCM
 #else
       const bool ms = h & 0x20u, is = h & 0x10u;
 #endif
-      const bool short0 = C0.win_switch_flag == 1 && C0.block_type == 2;
-      const bool mixed0 = C0.mixed_block_flag != 0;
+      const bool short0 = is_short(cp1[0]);
+      const bool mixed0 = (cp1[0] >> 24) != 0;
       const float inv_sqrt2 = 0.70710678118654752440f;
       if (ms) {
         // MS: L' = (l + r)c, R' = (l - r)c for lines below max(count1)
@@ -565,9 +576,9 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       }
     }
     {
-      const bool sw = C.win_switch_flag == 1 && C.block_type == 2;
-      const bool skip = !act || (sw && C.mixed_block_flag == 0);
-      const int sblim = (sw && C.mixed_block_flag == 1) ? 2 : 32;
+      const bool sw = shortblk;
+      const bool skip = !act || (sw && !mixed);
+      const int sblim = (sw && mixed) ? 2 : 32;
       const bool lower = !skip && k >= 1 && k < sblim;     // butterfly with subband k-1
       const bool upper = !skip && k < 31 && k + 1 < sblim;  // butterfly with subband k+1
       float up[8], dn[8];
@@ -592,8 +603,9 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     // ---- IMDCT + overlap + frequency inversion ----
     float o[18];
     {
-      int bt = C.block_type & 3;
-      if (C.win_switch_flag == 1 && C.mixed_block_flag == 1 && k < 2) bt = 0;
+      // mixed blocks: long windows for subbands 0, 1 whenever win_switch && mixed (frame.go:462-466)
+      int bt = (int)((d1 >> 16) & 3u);
+      if ((d1 & 0xff00ff00u) == 0x01000100u && k < 2) bt = 0;
       // raw[0..17] + old overlap -> o[], raw[18..35] -> new overlap, written as
       // each raw value is produced (no 36-entry temporary); frequency
       // inversion rides on the signs of the windows and of stp
