@@ -27,6 +27,8 @@
 // windows) -> 11 resident waves per CU.
 // (compiled as part of kernels.hip, after granule_common.hip)
 #pragma clang fp contract(fast)
+#include <type_traits>
+
 #include "dct32.h"
 #include "dct4_18.h"
 #include "xlane.h"
@@ -643,20 +645,29 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
         f2 P[9];
         dct4::dct4_18_pk(x, P);
         const float4* Wq = sh.winp[bt][lane_fresh() & 1];
+        // (the overlap of an absent channel stays frozen: frame.go Decode
+        // touches ch < nch only; stereo granules need no per-lane select)
+        auto overlap = [&](auto frozen) {
 #pragma unroll
-        for (int kk = 0; kk < 9; kk++) {
-          const int q = kk <= 4 ? 8 - 2 * kk : 2 * kk - 9;
-          const float za = kk <= 4 ? P[kk].y : P[kk].x;  // X[9+q]
-          const float zb = kk <= 4 ? P[kk].x : P[kk].y;  // X[8-q]
-          const float4 w = Wq[q];
-          // (o[q], o[17-q]) = X[9+q] (W[q], -W[17-q]) + stp[q];
-          // new stp[q] = X[8-q] (-W[18+q], -W[35-q])   (signs folded in w)
-          const f2 oq = pfma(bcast(za), (f2){w.x, w.y}, stp[q]);
-          o[q] = oq.x;
-          o[17 - q] = oq.y;
-          const f2 ns = bcast(zb) * (f2){w.z, w.w};
-          stp[q] = (f2){self(act, ns.x, stp[q].x), self(act, ns.y, stp[q].y)};
-        }
+          for (int kk = 0; kk < 9; kk++) {
+            const int q = kk <= 4 ? 8 - 2 * kk : 2 * kk - 9;
+            const float za = kk <= 4 ? P[kk].y : P[kk].x;  // X[9+q]
+            const float zb = kk <= 4 ? P[kk].x : P[kk].y;  // X[8-q]
+            const float4 w = Wq[q];
+            // (o[q], o[17-q]) = X[9+q] (W[q], -W[17-q]) + stp[q];
+            // new stp[q] = X[8-q] (-W[18+q], -W[35-q])   (signs folded in w)
+            const f2 oq = pfma(bcast(za), (f2){w.x, w.y}, stp[q]);
+            o[q] = oq.x;
+            o[17 - q] = oq.y;
+            const f2 ns = bcast(zb) * (f2){w.z, w.w};
+            if constexpr (decltype(frozen)::value)
+              stp[q] = (f2){self(act, ns.x, stp[q].x), self(act, ns.y, stp[q].y)};
+            else
+              stp[q] = ns;
+          }
+        };
+        if (nch == 2) overlap(std::false_type{});
+        else overlap(std::true_type{});
       }
     }
     stamp(3);
@@ -766,13 +777,18 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       // every lane stores one dword per slot pair and the wave 2 x 128
       // contiguous bytes.  Mono: the swap hands lane i channel 0's slot 2p and
       // lane 32 + i its slot 2p + 1, stored in both halves (frame.go:671-678).
+      auto pack = [&](auto mono) {
 #pragma unroll
-      for (int p = 0; p < 9; p++) {
-        const int a = (int)__builtin_amdgcn_fmed3f(acc2[p].x, -32767.0f, 32767.0f);
-        const int b = (int)__builtin_amdgcn_fmed3f(acc2[p].y, -32767.0f, 32767.0f);
-        const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
-        pk[p] = ((uint32_t)r[0] & 0xffffu) | ((uint32_t)(nch == 2 ? r[1] : r[0]) << 16);
-      }
+        for (int p = 0; p < 9; p++) {
+          const int a = (int)__builtin_amdgcn_fmed3f(acc2[p].x, -32767.0f, 32767.0f);
+          const int b = (int)__builtin_amdgcn_fmed3f(acc2[p].y, -32767.0f, 32767.0f);
+          const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+          // low halves of (r[0], r[1]) -> one dword: L | R << 16 (R = L for mono)
+          pk[p] = __builtin_amdgcn_perm((uint32_t)(decltype(mono)::value ? r[0] : r[1]), (uint32_t)r[0], 0x05040100u);
+        }
+      };
+      if (nch == 2) pack(std::false_type{});
+      else pack(std::true_type{});
       pend_g = g;
     }
     wave_sync();  // ring reads done
