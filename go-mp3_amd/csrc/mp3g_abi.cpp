@@ -115,6 +115,44 @@ uint32_t auto_chunk(const mp3g_stream* streams, uint32_t n_streams, int device, 
   return (uint32_t)std::min<uint64_t>(best_k, 1u << 20);
 }
 
+// Chunks per stream for a total of about `total` chunks: proportional to the
+// stream lengths, at least 1 and at most n_granules per non-empty stream.
+std::vector<uint64_t> spread_chunks(const mp3g_stream* streams, uint32_t n_streams, uint64_t total) {
+  uint64_t n = 0;
+  for (uint32_t s = 0; s < n_streams; s++) n += streams[s].n_granules;
+  std::vector<uint64_t> c(n_streams, 0);
+  for (uint32_t s = 0; s < n_streams; s++) {
+    const uint64_t ns = streams[s].n_granules;
+    if (!ns) continue;
+    const uint64_t want = (uint64_t)((double)ns * (double)total / (double)n + 0.5);
+    c[s] = std::min<uint64_t>(ns, std::max<uint64_t>(1, want));
+  }
+  return c;
+}
+
+// Automatic chunk counts.  The cost model's length k first; then, when the
+// plan fills at least half a round of resident chunks, the total is rounded up
+// to whole rounds (every wave slot of every round gets a chunk: on c2 the
+// model's 3,334 chunks put 4 workgroups on 66 CUs and 3 on the others, and
+// the 4-workgroup CUs set the launch time) and the streams are cut into
+// chunks of equal length.
+std::vector<uint64_t> auto_chunks(const mp3g_stream* streams, uint32_t n_streams, int device, uint32_t base_mode) {
+  const uint64_t k = auto_chunk(streams, n_streams, device, base_mode);
+  uint64_t c0 = 0;
+  for (uint32_t s = 0; s < n_streams; s++) c0 += (streams[s].n_granules + k - 1) / k;
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
+  const uint64_t resident =
+      (uint64_t)cus * (uint64_t)chunks_per_cu(base_mode == MP3G_MODE_FAST ? kVariantFast : kVariantV2);
+  if (2 * c0 < resident) {
+    std::vector<uint64_t> c(n_streams);
+    for (uint32_t s = 0; s < n_streams; s++) c[s] = (streams[s].n_granules + k - 1) / k;
+    return c;
+  }
+  const uint64_t rounds = (c0 + resident - 1) / resident;
+  return spread_chunks(streams, n_streams, rounds * resident);
+}
+
 }  // namespace
 
 int mp3g::abi_fail(int status, const char* what) { return fail(status, what); }
@@ -224,8 +262,17 @@ int mp3g_plan_create(int device, const mp3g_stream* streams, uint32_t n_streams,
   if (guard.err != hipSuccess) return fail(MP3G_ERR_NO_DEVICE, "hipSetDevice", guard.err);
   int st = ensure_device(device);
   if (st) return st;
-  uint32_t k = granules_per_chunk;
-  if (k == 0) k = auto_chunk(streams, n_streams, device, base_mode);
+  // chunks per stream (lengths within a stream differ by at most one)
+  std::vector<uint64_t> nc;
+  if (granules_per_chunk == 0) {
+    nc = auto_chunks(streams, n_streams, device, base_mode);
+  } else if (granules_per_chunk & 0x80000000u) {
+    nc = spread_chunks(streams, n_streams, std::max<uint32_t>(1, granules_per_chunk & 0x7fffffffu));
+  } else {
+    nc.resize(n_streams);
+    for (uint32_t s = 0; s < n_streams; s++)
+      nc[s] = (streams[s].n_granules + granules_per_chunk - 1) / granules_per_chunk;
+  }
   mp3g_plan* p = new (std::nothrow) mp3g_plan;
   if (!p) return fail(MP3G_ERR_OUT_OF_MEMORY, "plan");
   p->device = device;
@@ -233,17 +280,21 @@ int mp3g_plan_create(int device, const mp3g_stream* streams, uint32_t n_streams,
   p->n_streams = n_streams;
   for (uint32_t s = 0; s < n_streams; s++) {
     const mp3g_stream& S = streams[s];
-    for (uint64_t off = 0; off < S.n_granules; off += k) {
+    const uint64_t cs = nc[s];
+    for (uint64_t i = 0, off = 0; i < cs && off < S.n_granules; i++) {
+      // chunk i of cs: granules [i n / cs, (i + 1) n / cs)
+      const uint64_t next = (i + 1) * S.n_granules / cs;
       ChunkDesc c{};
       c.out_first = S.first_granule + off;
       c.stream_first = S.first_granule;
-      c.n_out = (uint32_t)std::min<uint64_t>(k, S.n_granules - off);
+      c.n_out = (uint32_t)(next - off);
       c.stream = s;
       c.flags = (S.flags & MP3G_STREAM_STATE_IN) ? kChunkStateIn : 0u;
       if ((S.flags & MP3G_STREAM_STATE_OUT) && off + c.n_out == S.n_granules) c.flags |= kChunkStateOut;
       p->chunks.push_back(c);
       p->n_granules += c.n_out;
       p->n_halo += std::min<uint64_t>(off, 2);
+      off = next;
     }
     if (S.n_granules == 0 && (S.flags & MP3G_STREAM_STATE_OUT)) {
       // empty stream exporting state: state_out = state_in (or zero)

@@ -430,6 +430,11 @@ class Decoder:
 class Plan:
     """Device-resident plan (mp3g_plan_*): execute on device pointers / torch tensors."""
 
+    @staticmethod
+    def chunks(c):
+        """granules_per_chunk value for about c chunks in total (MP3G_PLAN_CHUNKS)."""
+        return 0x80000000 | int(c)
+
     def __init__(self, streams, granules_per_chunk=0, mode=MODE_EXACT, device=0):
         streams = np.ascontiguousarray(streams, dtype=STREAM_DTYPE)
         self._h = C.c_void_p()

@@ -140,11 +140,16 @@ int mp3g_validate(const mp3g_granule* granules, const int16_t* coeffs,
                   uint64_t n_granules, uint64_t* bad_index);
 
 /* ---- plans: device-resident work decomposition ---------------------------
- * A plan splits every stream into chunks of `granules_per_chunk` granules
- * (0 = automatic) processed by independent workgroups.  A chunk that does not
- * start a stream re-derives its entry state from the two preceding granules
- * (bit-identical to serial decode; DESIGN.md "halo").  The plan lives on
- * `device` and can be executed many times (graph-capturable). */
+ * A plan splits every stream into chunks processed by independent waves /
+ * workgroups.  granules_per_chunk: k > 0 = chunks of k granules;
+ * 0 = automatic (a length from the launch-cost model, then the chunk count
+ * rounded to whole rounds of resident chunks and every stream cut into
+ * chunks of equal length +-1); MP3G_PLAN_CHUNKS(c) = about c chunks in total,
+ * spread over the streams by length, equal lengths +-1.  A chunk that does
+ * not start a stream re-derives its entry state from the two preceding
+ * granules (bit-identical to serial decode; DESIGN.md "halo").  The plan lives
+ * on `device` and can be executed many times (graph-capturable). */
+#define MP3G_PLAN_CHUNKS(c) (0x80000000u | (uint32_t)(c))
 typedef struct mp3g_plan mp3g_plan;
 int mp3g_plan_create(int device, const mp3g_stream* streams, uint32_t n_streams,
                      uint32_t granules_per_chunk, uint32_t mode, mp3g_plan** out_plan);

@@ -16,7 +16,8 @@ import torch  # noqa: E402
 import mp3g  # noqa: E402
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
-k = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+karg = sys.argv[2] if len(sys.argv) > 2 else "0"  # granules per chunk, or c<N>: N chunks in total
+k = mp3g.Plan.chunks(int(karg[1:])) if karg.startswith("c") else int(karg)
 d_g, d_c, d_pcm, streams = device_workload(cfg)
 plan = mp3g.Plan(streams, granules_per_chunk=k, mode=mp3g.MODE_FAST)
 s = torch.cuda.current_stream()
@@ -30,7 +31,7 @@ e1.record(s)
 torch.cuda.synchronize()
 kern_us = e0.elapsed_time(e1) / 20 * 1e3
 t = plan.debug_timeline(d_g, d_c, d_pcm).astype(np.int64)
-np.save(os.path.join(REPO, "gpurun_out", f"timeline_{cfg}_{k}.npy"), t)
+np.save(os.path.join(REPO, "gpurun_out", f"timeline_{cfg}_{karg}.npy"), t)
 t = (t - t[:, 0].min()) / 100.0  # 100 MHz ticks -> us
 q = lambda a: [round(float(np.percentile(a, p)), 2) for p in (0, 50, 90, 100)]
 print(json.dumps({"config": cfg, "chunks": len(t), "info": plan.info(), "kernel_us_events": round(kern_us, 2),
