@@ -35,7 +35,14 @@
 
 namespace mp3g {
 namespace v3 {
-constexpr int kWaves = 4;  // independent chunks (one per wave) per workgroup; they share the tables
+// Independent chunks (one per wave) per workgroup, sharing the read-only
+// tables.  8 waves: 2 workgroups (16 waves) per CU, the shared tables held
+// twice per CU instead of four times (2-3 % faster than 4-wave workgroups on
+// c2 and c3, tools/gpu_ab.sh; 16 waves measured the same).
+#ifndef MP3G_FAST_WG_WAVES
+#define MP3G_FAST_WG_WAVES 8
+#endif
+constexpr int kWaves = MP3G_FAST_WG_WAVES;  // independent chunks (one per wave) per workgroup; they share the tables
 namespace {
 
 using common::hdr_combo;
@@ -70,10 +77,10 @@ __device__ __forceinline__ int kPretab(int sfb) { return (int)((0x2fe95400000ull
 //  * the matrixing lane of slot u reads and writes its slot across the 32
 //    columns: consecutive lanes hit consecutive dwords;
 //  * 2 x 32 x 34 x 4 = 8,704 B per wave, which with the raw coefficients in
-//    registers (no LDS copy) brings a 4-wave workgroup to 40.5 KB: 4
+//    registers (no LDS copy) brings an 8-wave workgroup to 75 KB: 2
 //    workgroups = 16 waves per CU.
 constexpr int kHist = 16;
-// 4 workgroups of 4 waves per CU: <= 128 VGPRs (MI355X_MICROARCH.md register
+// 16 waves per CU: <= 128 VGPRs (MI355X_MICROARCH.md register
 // table) next to the 40.5 KB of LDS per workgroup
 #ifndef MP3G_FAST_WAVES_PER_SIMD
 #define MP3G_FAST_WAVES_PER_SIMD 4
@@ -94,8 +101,8 @@ struct __align__(16) SharedSmem {
   // granule's PCM stores
   uint32_t lband[kCombos][32];
 };
-// per-wave working set 9.1 KB.  The workgroup (4 waves + shared tables) must
-// stay <= 32 x 1280 B (gfx950 LDS allocation granule) for 4 workgroups
+// per-wave working set 9.1 KB.  The workgroup (8 waves + shared tables) must
+// stay <= 64 x 1280 B (gfx950 LDS allocation granule) for 2 workgroups
 // (16 waves) per CU.
 struct __align__(16) WaveSmem {
   // the current granule's slots of a column (16..33) first receive S (the

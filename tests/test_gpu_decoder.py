@@ -64,15 +64,21 @@ def test_random_seek_read_sequence(gpu, sample_files, mode):
             op = rng.integers(0, 6)
             if op < 3:
                 n = int(rng.choice([1, 3, 100, 4096, 4608, 20000, 300000]))
+                p = d.pos
                 st, b = d.read(n)
                 st2, b2 = o.read(n)
                 assert st == ST[st2] and len(b) == len(b2), (name, step, st, st2)
                 if mode != 1:
                     assert b == b2, (name, step)
                 elif b:
-                    diff = np.abs(np.frombuffer(b[:len(b) // 2 * 2], np.int16).astype(np.int32)
-                                  - np.frombuffer(b2[:len(b2) // 2 * 2], np.int16))
-                    assert diff.max(initial=0) <= 1
+                    # whole samples only, aligned to the stream (a read may start
+                    # or end inside a sample, whose byte alone says nothing
+                    # about a +-1 LSB difference)
+                    a0 = p % 2
+                    m = (len(b) - a0) // 2 * 2
+                    diff = np.abs(np.frombuffer(b[a0:a0 + m], np.int16).astype(np.int32)
+                                  - np.frombuffer(b2[a0:a0 + m], np.int16))
+                    assert diff.max(initial=0) <= 1, (name, step)
             elif op == 3:
                 whence = int(rng.integers(0, 3))
                 off = int(rng.integers(-L // 4, L + 10000))
