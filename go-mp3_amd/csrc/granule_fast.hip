@@ -205,17 +205,19 @@ __device__ __forceinline__ int seli(bool c, int a, int b) {
   return (a & m) | (b & ~m);
 }
 
-// sign(x) |x|^(4/3) 2^(n4/4) = ldexp(2^(4/3 log2|x| + (n4 & 3)/4), n4 >> 2), signed:
-// two transcendental VALU ops instead of the float64 table gather of the
-// reference (frame.go:148-155); relative error ~1e-6 (x = 0 -> exactly 0).
-// The band exponent arrives as e = n4 / 4 in float16 (exact: n4 is an integer
-// in [-390, 45], so e needs 11 significant bits), and the whole power goes
-// through one exp2: 2^(4/3 log2|x| + e).  For the values that reach the PCM
-// (|e| and |t| below ~32) the input rounding of t adds <= 2^-19 relative error.
+// sign(x) |x|^(4/3) 2^(n4/4) = x 2^(1/3 log2|x| + n4/4): two transcendental
+// VALU ops instead of the float64 table gather of the reference
+// (frame.go:148-155); relative error ~1e-6 (x = 0 -> exactly 0).  The factor
+// x carries the sign (a v_mul_f32 instead of the v_bfi_b32 of a copysign,
+// which issues at the slower VOP3 rate, tools/valu_cost.hip).  The band
+// exponent arrives as e = n4 / 4 in float16 (exact: n4 is an integer in
+// [-390, 45], so e needs 11 significant bits), and the power goes through one
+// exp2.  For the values that reach the PCM (|e| and |t| below ~32) the input
+// rounding of t adds <= 2^-19 relative error.
 __device__ __forceinline__ float requant_fast(int xi, _Float16 e) {
   const float xf = (float)xi;
-  const float t = __builtin_fmaf(__builtin_amdgcn_logf(fabsf(xf)), 4.0f / 3.0f, (float)e);
-  return copysignf(__builtin_amdgcn_exp2f(t), xf);
+  const float t = __builtin_fmaf(__builtin_amdgcn_logf(fabsf(xf)), 1.0f / 3.0f, (float)e);
+  return xf * __builtin_amdgcn_exp2f(t);
 }
 
 // The lane id, recomputed where it is used (asm volatile: not hoisted out of
@@ -451,18 +453,21 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
         xi[2 * q] = (int)(int16_t)(cw[q] & 0xffffu);
         xi[2 * q + 1] = (int)(int16_t)(cw[q] >> 16);
       }
-      // long band of line j: first band of the subband + band starts among lines 1..j
+      // long band of line j: first band of the subband + band starts among
+      // lines 1..j.  Every long band starts at an even line (consts.go:68-97
+      // SfBandIndices; dsp_tables.cpp checks it), so lines 2q and 2q + 1
+      // share one band: one exponent read per line pair.
       const uint32_t lb = sh.lband[combo][k];
-      _Float16 ex[18];
+      _Float16 ex[9];
 #pragma unroll
-      for (int j = 0; j < 18; j++)
-        ex[j] = s.expo[22 * ch + (int)(lb & 31u) + __builtin_popcount((lb >> 5) & ((2u << j) - 1u))];
+      for (int q = 0; q < 9; q++)
+        ex[q] = s.expo[22 * ch + (int)(lb & 31u) + __builtin_popcount((lb >> 5) & ((2u << (2 * q)) - 1u))];
       // Lines >= count1 hold zeros (the bitstream parse's guarantee,
       // maindata/huffman.go:130-134; mp3g_validate checks it), and requantizing
       // 0 gives 0, so long blocks need no per-line count1 test here.
       // (absent-channel lanes compute garbage that nothing reads)
 #pragma unroll
-      for (int j = 0; j < 18; j++) x[j] = requant_fast(xi[j], ex[j]);
+      for (int j = 0; j < 18; j++) x[j] = requant_fast(xi[j], ex[j >> 1]);
     } else {
       int nsfs = 0;  // short bands whose first line lies below count1 (frame.go:229-255 loop bound)
 #pragma unroll

@@ -18,7 +18,10 @@
 namespace mp3g {
 namespace huff {
 
-constexpr int kThreads = 256;
+#ifndef MP3G_HUFF_THREADS
+#define MP3G_HUFF_THREADS 256
+#endif
+constexpr int kThreads = MP3G_HUFF_THREADS;
 constexpr int kWaves = kThreads / 64;
 // Main data staged per wave: 64 consecutive jobs (16 MPEG-1 stereo frames)
 // span ~6.1 KB at 128 kbps.  7.5 KB per wave + the 9 KB of tables keep the

@@ -1,0 +1,16 @@
+#!/bin/bash
+# Build a variant of libmp3g.so with extra hipcc flags on one translation unit:
+#   tools/build_variant_tu.sh <tag> <kernels.hip|kernels_fast.hip> "<extra flags>"
+#   -> go-mp3_amd/mp3g/libmp3g_<tag>.so   (A/B on the GPU box through MP3G_LIB)
+set -eu
+TAG=$1; TU=$2; FLAGS=${3:-}
+C=$(cd "$(dirname "$0")/../go-mp3_amd/csrc" && pwd)
+make -s -C "$C" >/dev/null
+B=$C/build/var_$TAG; mkdir -p "$B"
+HIPCC=/opt/rocm/bin/hipcc
+CXXFLAGS="-O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize -Wall -Wno-unused-function --offload-arch=gfx950 -I$C/../../include"
+EXTRA=""; [ "$TU" = kernels_fast.hip ] && EXTRA="-mllvm -disable-machine-licm"
+$HIPCC $CXXFLAGS $EXTRA $FLAGS -c "$C/$TU" -o "$B/$TU.o"
+objs=$(ls "$C"/build/*.o | grep -v "/$TU.o")
+$HIPCC --offload-arch=gfx950 -shared -o "$C/../mp3g/libmp3g_$TAG.so" $objs "$B/$TU.o"
+echo "built libmp3g_$TAG.so"

@@ -10,7 +10,7 @@ tail -2 gpurun_out/ab_pytest.log
 for rep in 1 2; do
 for cfg in c3 c2; do
   for lib in "$@"; do
-    steps=10; [ $cfg = c2 ] && steps=50
+    steps=10; [ $cfg = c2 ] && steps=200
     MP3G_LIB=$L/$lib timeout -k 10 300 python bench.py --config $cfg --steps $steps --warmup 3 --single-mode --no-cpu-baseline --no-bitstream > gpurun_out/ab_${lib}_$cfg.log 2>&1 || { tail -5 gpurun_out/ab_${lib}_$cfg.log; exit 1; }
     tail -1 gpurun_out/ab_${lib}_$cfg.log | python -c "import json,sys;d=json.loads(sys.stdin.read());print('$cfg','$lib',d['value'],d['roofline']['kernel_ms'],d.get('max_dpcm_lsb'))"
   done
