@@ -342,22 +342,9 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
   }
   wave_sync();
 
-  // PCM of a granule is stored during the next granule's front end: a VMEM
-  // store's VGPRs may not be overwritten until it completes (the compiler
-  // puts an s_waitcnt vmcnt(0) before the first reuse), so stores issued at
-  // the end of a granule stalled the wave right after them.  pk[] = one dword
-  // (L, R) per lane and slot pair, pend_g = the granule they belong to.
+  // PCM of a granule: one dword (L, R) per lane and slot pair
   uint32_t pk[9];
-  uint32_t pend_g = ~0u;
   const int hi = lane >> 5;
-  auto store_pcm = [&]() {
-    if (pend_g != ~0u) {
-      uint32_t* P = reinterpret_cast<uint32_t*>(pcm + (size_t)pend_g * 1152);
-#pragma unroll
-      for (int p = 0; p < 9; p++) P[32 * (2 * p + hi) + k] = pk[p];
-      pend_g = ~0u;
-    }
-  };
 
   if constexpr (kStamp) {
     tprev = __builtin_amdgcn_s_memtime();
@@ -609,9 +596,6 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
         x[17 - i] = self(upper, li * cs - dn[i] * ca, li);
       }
     }
-    // the previous granule's PCM (see pk[]); after the stereo stage, whose
-    // table loads would otherwise wait for these stores (vmcnt is in order)
-    store_pcm();
 
     stamp(2);
     // ---- IMDCT + overlap + frequency inversion ----
@@ -801,7 +785,12 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       };
       if (nch == 2) pack(std::false_type{});
       else pack(std::true_type{});
-      pend_g = g;
+      // stored right away: a store's data registers are free again once it
+      // has issued (no s_waitcnt before their reuse on gfx950), and the loads
+      // this wave waits for next were issued before these stores
+      uint32_t* P = reinterpret_cast<uint32_t*>(pcm + (size_t)g * 1152);
+#pragma unroll
+      for (int p = 0; p < 9; p++) P[32 * (2 * p + hi) + k] = pk[p];
     }
     wave_sync();  // ring reads done
     stamp(6);
@@ -816,7 +805,6 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     wave_sync();
     stamp(7);
   }
-  store_pcm();
   if constexpr (kStamp) rt[2] = __builtin_amdgcn_s_memrealtime();
 
   if (cd.flags & kChunkStateOut) {
