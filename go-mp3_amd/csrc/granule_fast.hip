@@ -792,17 +792,23 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
 #pragma unroll
       for (int p = 0; p < 9; p++) P[32 * (2 * p + hi) + k] = pk[p];
     }
+#ifndef MP3G_EXP_NOSYNC_SHIFT
     wave_sync();  // ring reads done
+#endif
     stamp(6);
 
     // ---- history shift (channels this granule touched): lane = (c, column),
-    //      slots 18..33 -> 0..15 as 8-B moves ----
-    if (ch < nch) {
+    //      slots 18..33 -> 0..15 as 8-B moves; not after a replayed granule
+    //      whose V feeds nothing (its slots hold no X; the next granule is a
+    //      replay too and rewrites the history before any window reads it) ----
+    if (ch < nch && need_v) {
       f2* col = reinterpret_cast<f2*>(&s.ring[ch][k][0]);
 #pragma unroll
       for (int q = 0; q < 8; q++) col[q] = col[9 + q];
     }
+#ifndef MP3G_EXP_NOSYNC_SHIFT2
     wave_sync();
+#endif
     stamp(7);
   }
   if constexpr (kStamp) rt[2] = __builtin_amdgcn_s_memrealtime();
