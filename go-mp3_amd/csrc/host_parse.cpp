@@ -536,6 +536,31 @@ St read_header(Source& s, int64_t* pos_io, uint32_t* out) {  // frameheader.go:2
   return St::kOk;
 }
 
+void prescan(const uint8_t* data, size_t len, uint64_t* n_granules, uint64_t* md_bytes) {
+  *n_granules = *md_bytes = 0;
+  Source src;
+  src.data = data;
+  src.len = (int64_t)len;
+  if (src.skip_tags() != St::kOk) return;
+  uint8_t skip[2048];
+  for (;;) {  // the checks of FrameScanner::next that need no side info
+    uint32_t h;
+    int64_t pos = src.pos;
+    if (read_header(src, &pos, &h) != St::kOk) return;
+    const int crc = h_protection(h) == 0 ? 2 : 0;
+    if (h_id(h) == 0 || h_layer(h) != 1) return;
+    const int fsize = header_frame_size(h);
+    if (fsize < 0 || fsize > 2000) return;
+    const int sis = h_side_info_size(h);
+    const int size = fsize - sis - 4 - crc;
+    if (size > 1500 || size < 0) return;
+    bool sr;
+    if (src.read_full(skip, crc + sis + size, &sr) < crc + sis + size) return;
+    *n_granules += (uint64_t)header_granules(h);
+    *md_bytes += (uint64_t)size;
+  }
+}
+
 // ---- frame.Read (frame.go:67-115) + maindata.Read (maindata.go:85-117, :290-323) ----
 St FrameParser::next(Source& s, ParsedFrame* out) {
   std::call_once(g_lut_once, build_lut);
@@ -643,7 +668,27 @@ int64_t sf_end(int64_t pos, int64_t end, const mp3g_hjob& j) {
 
 }  // namespace
 
-St FrameScanner::next(Source& s, ScannedFrame* out, std::vector<uint8_t>* md) {
+namespace {
+// appends to the main-data sinks (n bytes in use afterwards)
+bool md_resize(std::vector<uint8_t>* v, size_t n) {
+  v->resize(n);
+  return true;
+}
+bool md_resize(RawMd* r, size_t n) {
+  if (n > r->cap) {
+    r->overflow = true;
+    return false;
+  }
+  r->n = n;
+  return true;
+}
+}  // namespace
+
+St FrameScanner::next(Source& s, ScannedFrame* out, std::vector<uint8_t>* md) { return next_impl(s, out, md); }
+St FrameScanner::next(Source& s, ScannedFrame* out, RawMd* md) { return next_impl(s, out, md); }
+
+template <class Md>
+St FrameScanner::next_impl(Source& s, ScannedFrame* out, Md* md) {
   // header, CRC, side info and sizes exactly as FrameParser::next
   uint32_t h;
   int64_t pos = s.pos;
@@ -675,10 +720,10 @@ St FrameScanner::next(Source& s, ScannedFrame* out, std::vector<uint8_t>* md) {
   const int offset = si.main_data_begin;
   const bool underflow = have_prev_ && offset > g0 - prev_start_;
   const int64_t vstart = !have_prev_ ? g0 : underflow ? prev_start_ : g0 - offset;
-  md->resize((size_t)(g0 + size));
+  if (!md_resize(md, (size_t)(g0 + size))) return St::kErr;
   bool sr;
   if (s.read_full(md->data() + g0, size, &sr) < size) {
-    md->resize((size_t)g0);
+    md_resize(md, (size_t)g0);
     return sr ? St::kEof : St::kErr;
   }
   const int64_t end = (int64_t)md->size() * 8;

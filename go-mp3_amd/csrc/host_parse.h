@@ -76,12 +76,26 @@ struct ScannedFrame {
   mp3g_hjob job[2][2];   // [gr][ch]; bit positions in the scanner's main-data buffer
 };
 
+// A main-data sink over caller memory: bytes [0, n) are in use, appends may
+// grow n up to cap (mp3g_scan_streams writes every stream's main data
+// straight into its place in the concatenation).  `overflow` records an
+// append that did not fit.
+struct RawMd {
+  uint8_t* base = nullptr;
+  size_t n = 0, cap = 0;
+  bool overflow = false;
+  size_t size() const { return n; }
+  uint8_t* data() const { return base; }
+};
+
 class FrameScanner {
  public:
   // Parses the next frame's header and side info and appends its main-data
   // bytes to *md; the same statuses, at the same source positions, as
-  // FrameParser::next on the same input.
+  // FrameParser::next on the same input.  (RawMd: a frame that does not fit
+  // ends the scan with kErr and sets md->overflow.)
   St next(Source& src, ScannedFrame* out, std::vector<uint8_t>* md);
+  St next(Source& src, ScannedFrame* out, RawMd* md);
   void reset() { have_prev_ = false; }  // frame.Read(source, pos, nil)
   // First byte of *md the next frame's bit buffer can reach back to.
   int64_t live_start(const std::vector<uint8_t>& md) const { return have_prev_ ? prev_start_ : (int64_t)md.size(); }
@@ -91,10 +105,18 @@ class FrameScanner {
  private:
   bool have_prev_ = false;
   int64_t prev_start_ = 0;  // byte offset in *md of the previous frame's bit buffer
+  template <class Md>
+  St next_impl(Source& src, ScannedFrame* out, Md* md);
 };
 
 // frameheader.Read: sync search from the source position.
 St read_header(Source& s, int64_t* pos_io, uint32_t* out);
+
+// Header-only walk of a whole stream (tags, sync search, sizes): the granules
+// and main-data bytes of the frames FrameScanner would accept if no frame's
+// side info ended the stream early (an upper bound; equal for every stream
+// that scans to EOF).
+void prescan(const uint8_t* data, size_t len, uint64_t* n_granules, uint64_t* md_bytes);
 
 // frameheader accessors used by the decoder
 int header_bytes_per_frame(uint32_t h);

@@ -3,6 +3,7 @@
 // host_parse.cpp FrameScanner) and mp3g_decode_streams (bitstreams in, PCM
 // out: the scan, then Huffman + DSP on the device).
 #include <hip/hip_runtime.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <atomic>
@@ -22,18 +23,38 @@ using host::St;
 
 namespace {
 
-// An uninitialised array (the merge overwrites every byte; zeroing hundreds
-// of MB first would cost as much as the copy).
+// An uninitialised array (the scan overwrites every byte; zeroing hundreds
+// of MB first would cost as much as writing them), in transparent huge pages
+// where the kernel offers them (madvise mode): the first touch of each fresh
+// 4-KB page costs about as much as filling it.
 template <class T>
 struct Buf {
-  std::unique_ptr<T[]> p;
-  size_t n = 0;
-  bool alloc(size_t count) {
-    p.reset(new (std::nothrow) T[std::max<size_t>(count, 1)]);
-    n = p ? count : 0;
-    return (bool)p;
+  T* p = nullptr;
+  size_t n = 0, bytes = 0;
+  Buf() = default;
+  Buf(const Buf&) = delete;
+  Buf& operator=(const Buf&) = delete;
+  ~Buf() { release(); }
+  void release() {
+    if (p) munmap(p, bytes);
+    p = nullptr;
+    n = bytes = 0;
   }
-  T* data() const { return p.get(); }
+  bool alloc(size_t count) {
+    release();
+    const size_t huge = size_t(2) << 20;
+    bytes = (std::max<size_t>(count, 1) * sizeof(T) + huge - 1) & ~(huge - 1);
+    void* q = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (q == MAP_FAILED) {
+      bytes = 0;
+      return false;
+    }
+    madvise(q, bytes, MADV_HUGEPAGE);  // advisory: 4-KB pages if refused
+    p = static_cast<T*>(q);
+    n = count;
+    return true;
+  }
+  T* data() const { return p; }
   size_t size() const { return n; }
   T& operator[](size_t i) const { return p[i]; }
 };
@@ -95,6 +116,42 @@ void scan_all(const uint8_t* data, size_t len, StreamScan* out) {
   out->end = st;
 }
 
+// The same scan written straight into the concatenation: granules from
+// gran[0], jobs from jobs[0], main data appended to *md (positions in the
+// jobs are then absolute).  Returns the granules written; more than `cap`
+// granules or main data past md->cap stops with *overflow set.
+uint64_t scan_into(const uint8_t* data, size_t len, mp3g_granule* gran, mp3g_hjob* jobs, uint64_t cap,
+                   host::RawMd* md, St* end, bool* overflow) {
+  host::Source src;
+  src.data = data;
+  src.len = (int64_t)len;
+  *overflow = false;
+  St st = src.skip_tags();
+  if (st != St::kOk) {
+    *end = st;
+    return 0;
+  }
+  host::FrameScanner sc;
+  host::ScannedFrame f;
+  uint64_t n = 0;
+  for (;;) {
+    st = sc.next(src, &f, md);
+    if (st != St::kOk) break;
+    if (n + (uint64_t)f.n_granules > cap) {
+      *overflow = true;
+      break;
+    }
+    for (int gr = 0; gr < f.n_granules; gr++, n++) {
+      gran[n] = f.gran[gr];
+      jobs[2 * n] = f.job[gr][0];
+      jobs[2 * n + 1] = f.job[gr][1];
+    }
+  }
+  *overflow = *overflow || md->overflow;
+  *end = st;
+  return n;
+}
+
 }  // namespace
 
 extern "C" {
@@ -118,6 +175,53 @@ int mp3g_scan_streams(uint32_t n_streams, const uint8_t* const* datas, const siz
     work();
     for (auto& t : pool) t.join();
   };
+  // Direct path: a header-only pre-pass sizes every stream, then each stream
+  // is scanned straight into its place in the concatenation (no per-stream
+  // buffers, no merge copy).  A stream whose side info ends it before the
+  // pre-pass's count (a parse error or a reference panic mid-stream) sends the
+  // batch to the two-step path below.
+  {
+    std::vector<uint64_t> pg(n_streams), pm(n_streams);
+    parallel([&](uint32_t k) { host::prescan(datas[k], lens[k], &pg[k], &pm[k]); });
+    std::vector<uint64_t> g_at(n_streams + 1), m_at(n_streams + 1);
+    for (uint32_t k = 0; k < n_streams; k++) {
+      g_at[k + 1] = g_at[k] + pg[k];
+      m_at[k + 1] = m_at[k] + ((pm[k] + 15) & ~(uint64_t)15);
+    }
+    const uint64_t ng = g_at[n_streams], nmd = m_at[n_streams];
+    if (!s->gran.alloc(ng) || !s->jobs.alloc(2 * ng) || !s->md.alloc(nmd + 16)) {
+      delete s;
+      return abi_fail(MP3G_ERR_OUT_OF_MEMORY, "scan buffers");
+    }
+    s->streams.resize(n_streams);
+    s->status.resize(n_streams);
+    std::atomic<bool> ok{true};
+    parallel([&](uint32_t k) {
+      host::RawMd md;
+      md.base = s->md.data();
+      md.n = m_at[k];
+      md.cap = m_at[k] + pm[k];
+      St end;
+      bool overflow;
+      const uint64_t n = scan_into(datas[k], lens[k], &s->gran[g_at[k]], &s->jobs[2 * g_at[k]], pg[k], &md, &end,
+                                   &overflow);
+      if (overflow || n != pg[k] || md.n != m_at[k] + pm[k]) {
+        ok = false;
+        return;
+      }
+      s->streams[k].first_granule = g_at[k];
+      s->streams[k].n_granules = (uint32_t)n;
+      s->streams[k].flags = 0;
+      s->status[k] = to_status(end);
+      std::memset(&s->md[md.n], 0, m_at[k + 1] + (k + 1 == n_streams ? 16 : 0) - md.n);
+    });
+    if (ok) {
+      *out = s;
+      return MP3G_OK;
+    }
+    s->streams.clear();
+    s->status.clear();
+  }
   parallel([&](uint32_t k) { scan_all(datas[k], lens[k], &per[k]); });
 
   // where each stream lands; each stream's main data 16-B aligned, 16 zero

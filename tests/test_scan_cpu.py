@@ -133,3 +133,46 @@ def test_jobs_synthetic(hjob_host):
     rng = np.random.default_rng(5)
     datas += mutations(datas[1], rng, 20)
     check_against_parse(hjob_host, datas, "synthetic")
+
+
+def _mpeg2_mixed_block(data):
+    """mpeg2.mp3 with the mixed-block flag set in the first granule of its
+    first short-block frame past frame 10 (MPEG-2 mono, no CRC): the
+    reference panics there (maindata.go:139-178)."""
+    b = bytearray(data)
+    off = 10 + ((b[6] << 21) | (b[7] << 14) | (b[8] << 7) | b[9])  # past the ID3v2 tag
+    brs = [0, 8, 16, 24, 32, 40, 48, 56, 64, 80, 96, 112, 128, 144, 160]
+    srs = [22050, 24000, 16000]
+    k = 0
+    while off + 4 < len(b):
+        h = int.from_bytes(b[off:off + 4], "big")
+        assert h >> 21 == 0x7FF and (h >> 19) & 3 == 2 and (h >> 6) & 3 == 3 and (h >> 16) & 1
+        size = (144 * brs[(h >> 12) & 15] * 1000 // srs[(h >> 10) & 3] + ((h >> 9) & 1)) >> 1
+        si = off + 4  # side info bits: win_switch 47, block_type 48-49, mixed 50
+        if k > 10 and b[si + 5] & 1 and b[si + 6] >> 6 == 2:
+            b[si + 6] |= 0x20
+            return bytes(b)
+        off += size
+        k += 1
+    raise AssertionError("no short block")
+
+
+def test_scan_direct_and_fallback_paths_agree(sample_files):
+    """mp3g_scan_streams writes each stream straight into the concatenation
+    sized by a header-only pre-pass; a stream that its side info ends early
+    (here an MPEG-2 mixed block: the reference panics) sends the batch to the
+    per-stream buffers + merge path.  Both give the same buffers for the
+    streams they share."""
+    from mp3g import synth
+    clean = [synth.encode_stream(5 + k, 40 + 17 * k) for k in range(5)] + [sample_files["classic_lame.mp3"]]
+    a = mp3g.scan_streams(clean, n_threads=3)  # direct path
+    bad = [_mpeg2_mixed_block(sample_files["mpeg2.mp3"])]
+    b = mp3g.scan_streams(clean + bad, n_threads=3)
+    assert b["end_status"][-1] == 8 and b["streams"][-1]["n_granules"] > 0  # ended early, after some frames
+    n = int(a["streams"][-1]["first_granule"] + a["streams"][-1]["n_granules"])
+    assert np.array_equal(a["streams"], b["streams"][:len(clean)])
+    assert np.array_equal(a["end_status"], b["end_status"][:len(clean)])
+    assert a["granules"].tobytes() == b["granules"][:n].tobytes()
+    assert a["jobs"].tobytes() == b["jobs"][:2 * n].tobytes()
+    md_end = (int(a["jobs"]["bit_end"].max()) + 7) // 8
+    assert a["main_data"][:md_end].tobytes() == b["main_data"][:md_end].tobytes()
