@@ -157,6 +157,19 @@ def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle):
     torch.cuda.synchronize(dev)
     pcie_s = time.perf_counter() - t
     plan.close()
+    # the product's pipelined drop-in, bitstream bytes in host memory -> PCM
+    # in (pinned) host memory: mp3g_decode_streams_into, groups of streams
+    # whose host scan overlaps the previous group's H2D, kernels and D2H
+    # (the first call allocates its staging and device buffers, the second
+    # reuses them: the time of the second)
+    pipe = []
+    for _ in range(2):
+        t = time.perf_counter()
+        n_p, _, st_p = mp3g.decode_streams_into(datas, hp, mode=mode, n_threads=16, device=idx)
+        pipe.append(time.perf_counter() - t)
+    assert n_p == n and all(x == 7 for x in st_p)
+    pipe_s = pipe[-1]
+    mp3g.lib().mp3g_release_cached_buffers()
     frames = n // 2
     md = int(s["main_data"].nbytes)
     out = {"workload": f"{cfg} as Layer III bitstreams: {n_streams} x {n_frames} frames, 44.1 kHz stereo "
@@ -172,9 +185,12 @@ def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle):
            "main_data_bytes": md, "bitstream_bytes": int(sum(len(d) for d in datas)),
            "host_scan_s": round(scan_s, 4), "host_scan_frames_per_s": round(frames / scan_s, 1),
            "host_scan_threads": 16, "writer_s": round(writer_s, 2),
-           # bitstream bytes in host memory -> PCM in host memory, the serial
-           # sum of the host scan and the PCIe-inclusive device leg (no overlap)
-           "end_to_end": {"frames_per_s": round(frames / (scan_s + pcie_s), 1),
+           # bitstream bytes in host memory -> PCM in host memory: the
+           # pipelined product call (measured), and for reference the serial
+           # sum of the host scan and the PCIe-inclusive device leg
+           "end_to_end": {"frames_per_s": round(frames / pipe_s, 1), "pipelined_s": round(pipe_s, 4),
+                          "api": "mp3g_decode_streams_into (16 host threads, pinned PCM out)",
+                          "serial_frames_per_s": round(frames / (scan_s + pcie_s), 1),
                           "host_scan_s": round(scan_s, 4), "h2d_huffman_dsp_d2h_s": round(pcie_s, 4),
                           "pcm_d2h_bytes": int(n * 2304)}}
     if check_oracle:

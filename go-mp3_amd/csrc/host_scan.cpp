@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <new>
 #include <thread>
 #include <vector>
@@ -152,9 +153,82 @@ uint64_t scan_into(const uint8_t* data, size_t len, mp3g_granule* gran, mp3g_hjo
   return n;
 }
 
+// fn(k) for k in [k0, k1) on up to nt threads (the calling thread included)
+template <class Fn>
+void parallel_for(uint32_t k0, uint32_t k1, int nt, Fn&& fn) {
+  std::atomic<uint32_t> next{k0};
+  auto work = [&]() {
+    for (uint32_t k; (k = next.fetch_add(1)) < k1;) fn(k);
+  };
+  nt = std::max(1, std::min<int>(nt, (int)(k1 - k0)));
+  std::vector<std::thread> pool;
+  for (int t = 1; t < nt; t++) pool.emplace_back(work);
+  work();
+  for (auto& t : pool) t.join();
+}
+
+// page-locked host memory and device memory that grow on demand
+struct Pinned {
+  void* p = nullptr;
+  size_t bytes = 0;
+  ~Pinned() {
+    if (p) (void)hipHostFree(p);
+  }
+  bool reserve(size_t b) {
+    if (b <= bytes) return true;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    bytes = 0;
+    if (hipHostMalloc(&p, b, hipHostMallocDefault) != hipSuccess) return false;
+    bytes = b;
+    return true;
+  }
+};
+struct DevMem {
+  void* p = nullptr;
+  size_t bytes = 0;
+  ~DevMem() {
+    if (p) (void)hipFree(p);
+  }
+  bool reserve(size_t b) {
+    if (b <= bytes) return true;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+    if (hipMalloc(&p, b) != hipSuccess) return false;
+    bytes = b;
+    return true;
+  }
+};
+
+// Staging and device buffers of mp3g_decode_streams_into, kept per device
+// between calls (grow-only; mp3g_release_cached_buffers frees them): a
+// multi-GB batch otherwise spends tens of ms pinning host memory and
+// allocating device memory in every call.  A call that finds its device's
+// set in use by another thread allocates its own.
+struct PipeBufs {
+  Pinned arena[2];
+  DevMem d_gran[2], d_jobs[2], d_md[2], d_coef[2], d_pcm[2];
+};
+std::mutex g_pipe_mu;
+std::vector<std::unique_ptr<PipeBufs>> g_pipe;  // [device]
+std::vector<bool> g_pipe_busy;
+
 }  // namespace
 
 extern "C" {
+
+void mp3g_release_cached_buffers(void) {
+  std::lock_guard<std::mutex> lk(g_pipe_mu);
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  for (size_t d = 0; d < g_pipe.size(); d++)
+    if (g_pipe[d] && !g_pipe_busy[d]) {
+      (void)hipSetDevice((int)d);
+      g_pipe[d].reset();
+    }
+  if (prev >= 0) (void)hipSetDevice(prev);
+}
 
 int mp3g_scan_streams(uint32_t n_streams, const uint8_t* const* datas, const size_t* lens, int n_threads,
                       mp3g_scan** out) {
@@ -351,6 +425,191 @@ int mp3g_decode_streams(int device, uint32_t n_streams, const uint8_t* const* da
   *pcm = host_pcm;
   *n_granules = n;
   return MP3G_OK;
+}
+
+int mp3g_decode_streams_into(int device, uint32_t n_streams, const uint8_t* const* datas, const size_t* lens,
+                             int n_threads, uint32_t mode, uint32_t n_groups, int16_t* pcm,
+                             uint64_t pcm_cap_granules, uint64_t* n_granules, mp3g_stream* streams,
+                             int* end_status) {
+  if (!n_granules || (n_streams && (!datas || !lens || !streams || !end_status)))
+    return abi_fail(MP3G_ERR_INVALID_ARGUMENT, "null argument");
+  *n_granules = 0;
+  const int nt = n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency();
+  // ---- the layout: a header-only pre-pass over every stream ----
+  std::vector<uint64_t> pg(n_streams), pm(n_streams), g_at(n_streams + 1), m_at(n_streams + 1);
+  parallel_for(0, n_streams, nt, [&](uint32_t k) { host::prescan(datas[k], lens[k], &pg[k], &pm[k]); });
+  for (uint32_t k = 0; k < n_streams; k++) {
+    g_at[k + 1] = g_at[k] + pg[k];
+    m_at[k + 1] = m_at[k] + ((pm[k] + 15) & ~(uint64_t)15);
+  }
+  const uint64_t total = g_at[n_streams];
+  *n_granules = total;
+  if (total > pcm_cap_granules) return abi_fail(MP3G_ERR_INVALID_ARGUMENT, "pcm holds fewer blocks than needed");
+  for (uint32_t k = 0; k < n_streams; k++) {
+    streams[k].first_granule = g_at[k];
+    streams[k].n_granules = 0;
+    streams[k].flags = 0;
+    end_status[k] = MP3G_OK;
+  }
+  if (total == 0) {
+    // streams with no frame: their scan statuses
+    for (uint32_t k = 0; k < n_streams; k++) {
+      host::Source src;
+      src.data = datas[k];
+      src.len = (int64_t)lens[k];
+      St st = src.skip_tags();
+      if (st == St::kOk) {
+        host::FrameScanner sc;
+        host::ScannedFrame f;
+        uint8_t one[1];
+        host::RawMd md;
+        md.base = one;
+        st = sc.next(src, &f, &md);
+      }
+      end_status[k] = to_status(st == St::kOk ? St::kErr : st);
+    }
+    return MP3G_OK;
+  }
+  if (!pcm) return abi_fail(MP3G_ERR_INVALID_ARGUMENT, "null pcm");
+
+  // ---- groups of consecutive streams with about equal granule counts ----
+  uint32_t G = n_groups ? n_groups : (uint32_t)std::min<uint64_t>(8, std::max<uint64_t>(1, total / 65536));
+  G = std::max(1u, std::min(G, n_streams));
+  std::vector<uint32_t> cut{0};
+  for (uint32_t k = 0; k < n_streams && cut.size() < G; k++)
+    if (g_at[k + 1] * G >= total * cut.size() && k + 1 < n_streams) cut.push_back(k + 1);
+  cut.push_back(n_streams);
+  const size_t ng_groups = cut.size() - 1;
+  uint64_t max_ng = 0, max_md = 0;
+  for (size_t gi = 0; gi < ng_groups; gi++) {
+    max_ng = std::max(max_ng, g_at[cut[gi + 1]] - g_at[cut[gi]]);
+    max_md = std::max(max_md, m_at[cut[gi + 1]] - m_at[cut[gi]]);
+  }
+  // pinned arena per slot: [granules | jobs | main data + 16]
+  const size_t b_gran = max_ng * sizeof(mp3g_granule), b_jobs = 2 * max_ng * sizeof(mp3g_hjob);
+  const size_t b_md = max_md + 16;
+
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  if (hipSetDevice(device) != hipSuccess) return abi_fail(MP3G_ERR_NO_DEVICE, "decode_streams_into: device");
+  int rc = MP3G_OK;
+  // this device's cached buffer set, or a private one if it is in use
+  std::unique_ptr<PipeBufs> own;
+  PipeBufs* B = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_pipe_mu);
+    if ((size_t)device >= g_pipe.size()) {
+      g_pipe.resize((size_t)device + 1);
+      g_pipe_busy.resize((size_t)device + 1, false);
+    }
+    if (!g_pipe_busy[(size_t)device]) {
+      if (!g_pipe[(size_t)device]) g_pipe[(size_t)device].reset(new (std::nothrow) PipeBufs);
+      B = g_pipe[(size_t)device].get();
+      if (B) g_pipe_busy[(size_t)device] = true;
+    }
+  }
+  if (!B) {
+    own.reset(new (std::nothrow) PipeBufs);
+    B = own.get();
+  }
+  if (!B) return abi_fail(MP3G_ERR_OUT_OF_MEMORY, "decode_streams_into: buffers");
+  {
+    Pinned* arena = B->arena;
+    DevMem *d_gran = B->d_gran, *d_jobs = B->d_jobs, *d_md = B->d_md, *d_coef = B->d_coef, *d_pcm = B->d_pcm;
+    hipStream_t st = nullptr;
+    hipEvent_t done[2] = {nullptr, nullptr};
+    std::vector<mp3g_plan*> plans(ng_groups, nullptr);
+    hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+    for (int i = 0; i < 2 && e == hipSuccess; i++) e = hipEventCreateWithFlags(&done[i], hipEventDisableTiming);
+    for (int i = 0; i < 2 && e == hipSuccess; i++) {
+      const bool ok = arena[i].reserve(b_gran + b_jobs + b_md) && d_gran[i].reserve(b_gran) &&
+                      d_jobs[i].reserve(b_jobs) && d_md[i].reserve(b_md) &&
+                      d_coef[i].reserve(max_ng * MP3G_COEF_PER_GRANULE * sizeof(int16_t)) &&
+                      d_pcm[i].reserve(max_ng * MP3G_PCM_BYTES_PER_GRANULE);
+      if (!ok) e = hipErrorOutOfMemory;
+    }
+    if (e != hipSuccess) rc = abi_fail(MP3G_ERR_DEVICE, "decode_streams_into: buffers");
+    for (size_t gi = 0; gi < ng_groups && rc == MP3G_OK; gi++) {
+      const int slot = (int)(gi & 1);
+      if (gi >= 2 && hipEventSynchronize(done[slot]) != hipSuccess) {  // the slot's previous group is done
+        rc = abi_fail(MP3G_ERR_DEVICE, "decode_streams_into: device");
+        break;
+      }
+      const uint32_t k0 = cut[gi], k1 = cut[gi + 1];
+      const uint64_t G0 = g_at[k0], M0 = m_at[k0], ng = g_at[k1] - G0, nmd = m_at[k1] - M0;
+      auto* gran = static_cast<mp3g_granule*>(arena[slot].p);
+      auto* jobs = reinterpret_cast<mp3g_hjob*>(static_cast<uint8_t*>(arena[slot].p) + b_gran);
+      uint8_t* md = static_cast<uint8_t*>(arena[slot].p) + b_gran + b_jobs;
+      // host scan of the group straight into the pinned arena (jobs address
+      // the group's main data; the previous group's transfers and kernels run
+      // meanwhile)
+      std::vector<mp3g_stream> local(k1 - k0);
+      std::atomic<bool> holes{false}, overflow{false};
+      parallel_for(k0, k1, nt, [&](uint32_t k) {
+        host::RawMd sink;
+        sink.base = md;
+        sink.n = m_at[k] - M0;
+        sink.cap = sink.n + pm[k];
+        St end;
+        bool ovf;
+        mp3g_granule* g = gran + (g_at[k] - G0);
+        mp3g_hjob* j = jobs + 2 * (g_at[k] - G0);
+        const uint64_t n = scan_into(datas[k], lens[k], g, j, pg[k], &sink, &end, &ovf);
+        if (ovf) overflow = true;
+        if (n < pg[k]) {  // ended early: the rest of its range decodes nothing
+          holes = true;
+          std::memset(static_cast<void*>(j + 2 * n), 0, (size_t)(2 * (pg[k] - n)) * sizeof(mp3g_hjob));
+        }
+        local[k - k0] = {g_at[k] - G0, (uint32_t)n, 0};
+        streams[k].n_granules = (uint32_t)n;
+        end_status[k] = to_status(end);
+        std::memset(md + sink.n, 0, (size_t)(m_at[k + 1] - M0 - sink.n));
+      });
+      std::memset(md + nmd, 0, 16);
+      if (overflow) {  // the pre-pass is an upper bound, so this cannot happen
+        rc = abi_fail(MP3G_ERR_INVALID_ARGUMENT, "decode_streams_into: layout");
+        break;
+      }
+      rc = mp3g_plan_create(device, local.data(), k1 - k0, 0, mode, &plans[gi]);
+      if (rc) break;
+      e = hipMemcpyAsync(d_gran[slot].p, gran, ng * sizeof(mp3g_granule), hipMemcpyHostToDevice, st);
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(d_jobs[slot].p, jobs, 2 * ng * sizeof(mp3g_hjob), hipMemcpyHostToDevice, st);
+      if (e == hipSuccess) e = hipMemcpyAsync(d_md[slot].p, md, nmd + 16, hipMemcpyHostToDevice, st);
+      if (e == hipSuccess && holes)
+        e = hipMemsetAsync(d_pcm[slot].p, 0, ng * MP3G_PCM_BYTES_PER_GRANULE, st);
+      if (e != hipSuccess) {
+        rc = abi_fail(MP3G_ERR_DEVICE, "decode_streams_into: H2D");
+        break;
+      }
+      rc = mp3g_huffman_execute(device, static_cast<const mp3g_hjob*>(d_jobs[slot].p), ng,
+                                static_cast<const uint8_t*>(d_md[slot].p), static_cast<mp3g_granule*>(d_gran[slot].p),
+                                static_cast<int16_t*>(d_coef[slot].p), st);
+      if (rc == MP3G_OK)
+        rc = mp3g_plan_execute(plans[gi], static_cast<const mp3g_granule*>(d_gran[slot].p),
+                               static_cast<const int16_t*>(d_coef[slot].p), nullptr, nullptr,
+                               static_cast<int16_t*>(d_pcm[slot].p), st);
+      if (rc) break;
+      e = hipMemcpyAsync(pcm + G0 * (MP3G_PCM_BYTES_PER_GRANULE / sizeof(int16_t)), d_pcm[slot].p,
+                         ng * MP3G_PCM_BYTES_PER_GRANULE, hipMemcpyDeviceToHost, st);
+      if (e == hipSuccess) e = hipEventRecord(done[slot], st);
+      if (e != hipSuccess) rc = abi_fail(MP3G_ERR_DEVICE, "decode_streams_into: D2H");
+    }
+    if (st && hipStreamSynchronize(st) != hipSuccess && rc == MP3G_OK)
+      rc = abi_fail(MP3G_ERR_DEVICE, "decode_streams_into: device");
+    for (mp3g_plan* p : plans)
+      if (p) mp3g_plan_destroy(p);
+    for (hipEvent_t ev : done)
+      if (ev) (void)hipEventDestroy(ev);
+    if (st) (void)hipStreamDestroy(st);
+  }
+  if (!own) {
+    std::lock_guard<std::mutex> lk(g_pipe_mu);
+    g_pipe_busy[(size_t)device] = false;
+  }
+  own.reset();
+  if (prev >= 0) (void)hipSetDevice(prev);
+  return rc;
 }
 
 }  // extern "C"

@@ -101,6 +101,10 @@ def lib():
         L.mp3g_huffman_execute.argtypes = [C.c_int, vp, u64, vp, vp, vp, vp]
         L.mp3g_decode_streams.argtypes = [C.c_int, u32, vp, vp, C.c_int, u32, C.POINTER(vp), C.POINTER(u64),
                                           vp, vp]
+        L.mp3g_decode_streams_into.argtypes = [C.c_int, u32, vp, vp, C.c_int, u32, u32, vp, u64, C.POINTER(u64),
+                                               vp, vp]
+        L.mp3g_release_cached_buffers.argtypes = []
+        L.mp3g_release_cached_buffers.restype = None
         L.mp3g_decoder_new.argtypes = [vp, sz, C.c_int, C.c_int, u32, C.POINTER(vp)]
         L.mp3g_decoder_free.argtypes = [vp]
         L.mp3g_decoder_read.argtypes = [vp, vp, sz, C.POINTER(sz)]
@@ -358,6 +362,26 @@ def decode_streams(datas, mode=MODE_EXACT, n_threads=0, device=0):
                                      _ptr(streams), _ptr(status)))
     k = n.value
     return _take(pcm, k, np.int16, (k, 576, 2)), streams, status[:len(datas)]
+
+
+def decode_streams_into(datas, out, mode=MODE_EXACT, n_threads=0, n_groups=0, device=0):
+    """Pipelined bitstreams-in, PCM-out (mp3g_decode_streams_into): groups of
+    streams, each group's host scan overlapping the previous group's
+    transfers and kernels.  `out` is a writable int16 buffer (numpy array or
+    a pinned torch tensor) of at least 1152 * (total granules) samples; the
+    layout comes from a header-only pre-pass (streams[k].first_granule).
+    Returns (n_granules, streams, end_status)."""
+    bufs, ptrs, lens = _stream_args(datas)
+    streams = np.zeros(len(datas), STREAM_DTYPE)
+    status = np.zeros(max(1, len(datas)), np.int32)
+    n = C.c_uint64()
+    if hasattr(out, "data_ptr"):
+        ptr, cap = out.data_ptr(), out.numel() // 1152
+    else:
+        ptr, cap = out.ctypes.data, out.size // 1152
+    _check(lib().mp3g_decode_streams_into(device, len(datas), ptrs, lens, n_threads, mode, n_groups,
+                                          C.c_void_p(ptr), cap, C.byref(n), _ptr(streams), _ptr(status)))
+    return n.value, streams, status[:len(datas)]
 
 
 class Decoder:

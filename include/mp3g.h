@@ -268,6 +268,26 @@ int mp3g_decode_streams(int device, uint32_t n_streams, const uint8_t* const* da
                         int n_threads, uint32_t mode, int16_t** pcm, uint64_t* n_granules,
                         mp3g_stream* streams, int* end_status);
 
+/* The same into caller memory, pipelined: the streams are decoded in groups
+ * and each group's host scan overlaps the transfers and kernels of the group
+ * before it.  The output layout comes from a header-only pre-pass: stream k
+ * starts at block streams[k].first_granule of `pcm` (576 stereo s16 samples
+ * per block); a stream its side info ends early (a parse error or a
+ * reference panic after its last good frame) decodes its n_granules blocks
+ * and leaves the rest of its range zero.  `pcm` (host memory; pinned memory
+ * keeps the device-to-host copies at PCIe speed and asynchronous) must hold
+ * pcm_cap_granules blocks; if that is too few, nothing is decoded and the
+ * call returns MP3G_ERR_INVALID_ARGUMENT with *n_granules = the blocks
+ * needed.  n_groups = 0 picks the group count. */
+int mp3g_decode_streams_into(int device, uint32_t n_streams, const uint8_t* const* datas, const size_t* lens,
+                             int n_threads, uint32_t mode, uint32_t n_groups, int16_t* pcm,
+                             uint64_t pcm_cap_granules, uint64_t* n_granules, mp3g_stream* streams,
+                             int* end_status);
+
+/* mp3g_decode_streams_into keeps its staging (page-locked) and device
+ * buffers per device between calls; this frees them (idle sets only). */
+void mp3g_release_cached_buffers(void);
+
 /* ---- decoder: mp3.NewDecoder / io.Reader / io.Seeker (decode.go:27-388) ----
  * Scans on the host with read-ahead (headers, side info, reservoir) and
  * decodes batches of frames on `device`: scale factors + Huffman codes with

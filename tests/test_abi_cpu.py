@@ -134,3 +134,24 @@ def test_exact_kernel_has_no_fma():
         assert "v_mul_f32" in body and "v_add_f32" in body, name
         bad = re.findall(r"\b(v_fma\w*|v_fmac\w*|v_mac_\w*|v_mad_\w*f32|v_pk_fma\w*)\b", body)
         assert not bad, (name, sorted(set(bad)))
+
+
+def test_decode_streams_into_capacity_check_needs_no_device(sample_files):
+    """mp3g_decode_streams_into sizes the output with its header pre-pass
+    before it touches a device: too small an output fails with the blocks
+    needed (here on the CPU, without a GPU)."""
+    import ctypes as C
+    import numpy as np
+    datas = [sample_files["classic_lame.mp3"], sample_files["mpeg2.mp3"]]
+    bufs = [np.frombuffer(d, np.uint8) for d in datas]
+    ptrs = (C.c_void_p * 2)(*[b.ctypes.data for b in bufs])
+    lens = (C.c_size_t * 2)(*[len(d) for d in datas])
+    n = C.c_uint64()
+    streams = np.zeros(2, mp3g.STREAM_DTYPE)
+    status = np.zeros(2, np.int32)
+    out = np.zeros(1152, np.int16)
+    rc = mp3g.lib().mp3g_decode_streams_into(0, 2, ptrs, lens, 2, mp3g.MODE_EXACT, 0, C.c_void_p(out.ctypes.data),
+                                              1, C.byref(n), streams.ctypes.data_as(C.c_void_p),
+                                              status.ctypes.data_as(C.c_void_p))
+    assert rc == 1  # MP3G_ERR_INVALID_ARGUMENT
+    assert n.value == 385 * 2 + 2872  # every frame of both streams: MPEG-1 two granules, MPEG-2 one

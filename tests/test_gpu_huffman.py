@@ -122,3 +122,34 @@ def test_bitstream_path_synthetic_vs_oracle(gpu):
         lo, m = int(streams[k]["first_granule"]), int(streams[k]["n_granules"])
         assert ost == oracle.ORC_OK and st[k] == 7
         assert pcm[lo:lo + m].tobytes() == opcm, k
+
+
+@pytest.mark.parametrize("n_groups", [1, 3, 0])
+def test_decode_streams_into_pipelined(gpu, sample_files, n_groups):
+    """mp3g_decode_streams_into (groups of streams, each group's host scan
+    overlapping the previous group's transfers and kernels) gives every
+    stream the PCM mp3g_decode_streams gives it, at the pre-pass layout; a
+    stream its side info ends early (MPEG-2 mixed block: reference panic)
+    decodes its frames before that point and leaves the rest of its range 0."""
+    import torch
+    from mp3g import synth
+    from test_scan_cpu import _mpeg2_mixed_block
+    datas = [synth.encode_stream(21 + k, 50 + 13 * k) for k in range(7)]
+    datas += [sample_files["classic_lame.mp3"], _mpeg2_mixed_block(sample_files["mpeg2.mp3"]),
+              sample_files["mpeg2.mp3"], b"", b"\x00" * 300]
+    want, ws, wst = gpu.decode_streams(datas, mode=gpu.MODE_EXACT)
+    with pytest.raises(gpu.Mp3gError):
+        gpu.decode_streams_into(datas, np.zeros(1152, np.int16))
+    out = torch.full((sum(int(x["n_granules"]) for x in ws) * 1152 + 10 * 1152 * 2000,), 0x5A5A,
+                     dtype=torch.int16).pin_memory()
+    n, s, st = gpu.decode_streams_into(datas, out, mode=gpu.MODE_EXACT, n_groups=n_groups)
+    pcm = out.numpy()[:n * 1152].reshape(n, 576, 2)
+    assert list(st) == list(wst)
+    assert list(s["n_granules"]) == list(ws["n_granules"])
+    for k in range(len(datas)):
+        lo, m = int(s[k]["first_granule"]), int(s[k]["n_granules"])
+        wlo = int(ws[k]["first_granule"])
+        assert np.array_equal(pcm[lo:lo + m], want[wlo:wlo + m]), k
+        hi = int(s[k + 1]["first_granule"]) if k + 1 < len(datas) else n
+        assert not pcm[lo + m:hi].any(), k  # the unused rest of an early-ended stream's range
+    assert st[8] == 8 and 0 < s[8]["n_granules"] < s[9]["n_granules"]
