@@ -7,7 +7,8 @@
 // filled) and the channel's 576 int16 coefficients (huffman_job.h).
 // Decoding inside a channel is bit-serial; the parallelism is across jobs
 // (two per granule, 64 per wave).  A wave's 64 consecutive jobs read one
-// contiguous span of the main data: the wave stages it in LDS with coalesced
+// contiguous span of the main data (huffman_sorted_kernel, the one launched:
+// a block's 256 jobs ranked by big_values and its whole span staged): the wave stages it in LDS with coalesced
 // 8-byte loads (byte-swapped once), so the bit-serial loop never waits on
 // global memory (on gfx9 a load's vmcnt wait would also wait for the
 // coefficient stores issued before it).  The Huffman tables (huff_lut.h,
@@ -105,14 +106,128 @@ huffman_kernel(const mp3g_hjob* __restrict__ jobs, uint64_t n_jobs, const uint8_
   }
 }
 
+
+#ifndef MP3G_HUFF_SORT
+#define MP3G_HUFF_SORT 1
+#endif
+// Block-sorted kernel (the one launched; huffman_kernel above is kept for
+// A/B runs, MP3G_HUFF_SORT=0): the 256 jobs of a block are ranked by
+// big_values (counting sort in LDS, bins of 4 pairs) before they are dealt to
+// lanes, so each wave's 64 lanes run big-values loops of similar length (the
+// loop of a wave lasts as long as its longest job).  The block's main-data
+// span is staged once for all four waves (a lane's job can sit anywhere in
+// it).  28 KB of staging + 9 KB of tables and <= 128 VGPRs keep 4 blocks (16
+// waves) per CU: c3 3.09 -> 2.78 ms, c2 142 -> 129 us.  The gain is modest
+// because a lane is bound by its own dependent chain (window -> LUT lookup in
+// LDS -> shift), not by idle lanes; 512-thread blocks (better sort, shared
+// tables) were 3 % faster at c3 and 6 % slower at c2.
+#ifndef MP3G_HUFF_BLOCK_STAGE_WORDS
+#define MP3G_HUFF_BLOCK_STAGE_WORDS 3584  // 28 KB: 256 jobs span ~25 KB at 128 kbps
+#endif
+constexpr int kBlockStage = MP3G_HUFF_BLOCK_STAGE_WORDS;
+constexpr int kBins = 128;  // bin 0: jobs that read nothing; 1 + big_values / 4 <= 73
+
+#ifndef MP3G_HUFF_MAXVGPR
+#define MP3G_HUFF_MAXVGPR 128  // unbounded, the compiler takes 129 (3 waves per SIMD)
+#endif
+#define MP3G_HUFF_SORTED_ATTR __attribute__((amdgpu_num_vgpr(MP3G_HUFF_MAXVGPR)))
+__global__ void __launch_bounds__(kThreads) MP3G_HUFF_SORTED_ATTR
+huffman_sorted_kernel(const mp3g_hjob* __restrict__ jobs, uint64_t n_jobs, const uint8_t* __restrict__ md,
+                      mp3g_granule* __restrict__ gran, int16_t* __restrict__ coef) {
+  static_assert(kThreads <= 1024 && kThreads % 64 == 0, "block shape");
+  __shared__ uint32_t T2[kHuffMaxEntries / 2];
+  __shared__ uint32_t s_root[34], s_lin[34];
+  __shared__ uint64_t stage[kBlockStage + 4];  // + 4: the LDS reader's look-ahead
+  __shared__ uint32_t s_bin[kBins];
+  __shared__ uint16_t s_order[kThreads];
+  __shared__ uint64_t s_lo[kWaves], s_hi[kWaves];
+  const uint32_t t = threadIdx.x;
+  const int lane = (int)(t & 63u), wv = (int)(t >> 6);
+  const uint32_t n_w = (g_huff.n_entries + 1) / 2;
+  const uint32_t* src_e = reinterpret_cast<const uint32_t*>(g_huff.e);
+  for (uint32_t i = t; i < n_w; i += kThreads) T2[i] = src_e[i];
+  const uint16_t* T = reinterpret_cast<const uint16_t*>(T2);
+  if (t < 34) {
+    s_root[t] = g_huff.root[t];
+    s_lin[t] = g_huff.linbits[t];
+  }
+  for (uint32_t i = t; i < (uint32_t)kBins; i += kThreads) s_bin[i] = 0u;
+  const uint64_t j0 = (uint64_t)blockIdx.x * kThreads;
+  uint32_t bin = 0u;
+  {
+    const uint64_t jt = j0 + t;
+    mp3g_hjob J{};
+    if (jt < n_jobs) J = jobs[jt];
+    const bool reads = jt < n_jobs && J.sf_kind != MP3G_SF_NONE;
+    const uint64_t base = job_base(J);
+    const uint64_t lo = wave_min(reads ? base : ~0ull);
+    const uint64_t hi = wave_max(reads ? J.bit_end : 0ull);
+    if (lane == 0) {
+      s_lo[wv] = lo;
+      s_hi[wv] = hi;
+    }
+    if (reads) bin = 1u + (J.big_values < 288u ? J.big_values : 288u) / 4u;
+  }
+  __syncthreads();
+  const uint32_t rank = atomicAdd(&s_bin[bin], 1u);
+  uint64_t lo = ~0ull, hi = 0ull;
+#pragma unroll
+  for (int w = 0; w < kWaves; w++) {
+    lo = s_lo[w] < lo ? s_lo[w] : lo;
+    hi = s_hi[w] > hi ? s_hi[w] : hi;
+  }
+  __syncthreads();
+  if (t < 64) {  // exclusive scan of the bins, two per lane
+    const uint32_t a = s_bin[2 * t], b = s_bin[2 * t + 1];
+    uint32_t inc = a + b;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(inc, o, 64);
+      inc += lane >= o ? u : 0u;
+    }
+    const uint32_t ex = inc - (a + b);
+    s_bin[2 * t] = ex;
+    s_bin[2 * t + 1] = ex + a;
+  }
+  const uint64_t nwords = hi > lo && lo != ~0ull ? ((hi - lo + 63) >> 6) : 0ull;
+  const bool staged = nwords <= (uint64_t)kBlockStage;  // block-uniform
+  if (staged) {
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(md + (lo >> 3));
+    for (uint32_t k = t; k < (uint32_t)nwords; k += kThreads) stage[k] = bswap64(src[k]);
+  }
+  __syncthreads();
+  s_order[s_bin[bin] + rank] = (uint16_t)t;
+  __syncthreads();
+  const uint64_t j = j0 + s_order[t];
+  int z = MP3G_LINES;  // first line this lane's row still needs zeroed
+  if (j < n_jobs) {
+    const mp3g_hjob J = jobs[j];
+    if (staged) {
+      // clamped as in huffman_kernel: a corrupt part 2 can start past the span
+      const uint64_t off64 = J.sf_kind != MP3G_SF_NONE ? (job_base(J) - lo) >> 6 : 0ull;
+      const uint32_t off = (uint32_t)(off64 < nwords ? off64 : nwords);
+      z = decode_job<false>(J, j, &stage[off], (uint32_t)nwords - off, gran, coef, T, s_root, s_lin);
+    } else {
+      z = decode_job_direct(J, j, md, gran, coef, T, s_root, s_lin);
+    }
+  }
+  // zero tails of the wave's 64 rows, one row at a time with the whole wave
+  for (int rr = 0; rr < 64; rr++) {
+    const int zr = __shfl(z, rr, 64);
+    if (zr >= MP3G_LINES) continue;  // wave-uniform
+    const uint64_t jr = ((uint64_t)__shfl((uint32_t)(j >> 32), rr, 64) << 32) | __shfl((uint32_t)j, rr, 64);
+    uint4* row = reinterpret_cast<uint4*>(coef + jr * MP3G_LINES);
+    for (int s8 = (zr >> 3) + lane; s8 < MP3G_LINES / 8; s8 += 64) row[s8] = make_uint4(0u, 0u, 0u, 0u);
+  }
+}
+
 }  // namespace huff
 
 hipError_t launch_huffman(const mp3g_hjob* d_jobs, uint64_t n_jobs, const uint8_t* d_md, mp3g_granule* d_gran,
                           int16_t* d_coef, hipStream_t stream) {
   if (n_jobs == 0) return hipSuccess;
   const uint64_t blocks = (n_jobs + huff::kThreads - 1) / huff::kThreads;
-  hipLaunchKernelGGL(huff::huffman_kernel, dim3((uint32_t)blocks), dim3(huff::kThreads), 0, stream, d_jobs, n_jobs,
-                     d_md, d_gran, d_coef);
+  hipLaunchKernelGGL(MP3G_HUFF_SORT ? huff::huffman_sorted_kernel : huff::huffman_kernel, dim3((uint32_t)blocks),
+                     dim3(huff::kThreads), 0, stream, d_jobs, n_jobs, d_md, d_gran, d_coef);
   return hipGetLastError();
 }
 

@@ -251,9 +251,7 @@ int mp3g_plan_create(int device, const mp3g_stream* streams, uint32_t n_streams,
   const uint32_t base_mode = mode & 0xffu;
   if (base_mode != MP3G_MODE_EXACT && base_mode != MP3G_MODE_FAST)
     return fail(MP3G_ERR_UNSUPPORTED, "mode not available");
-  uint64_t total = 0;
   for (uint32_t s = 0; s < n_streams; s++) {
-    total += streams[s].n_granules;
     // the fast kernel indexes granules with 32-bit wave-uniform scalars
     if (base_mode == MP3G_MODE_FAST && streams[s].first_granule + streams[s].n_granules >= (1ull << 32))
       return fail(MP3G_ERR_UNSUPPORTED, "fast mode: granule index >= 2^32");

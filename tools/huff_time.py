@@ -1,0 +1,58 @@
+"""Times the Huffman kernel alone on the c2 and c3 bitstreams (experiments:
+MP3G_LIB selects a variant library, tools/build_variant_tu.sh).
+
+  python tools/huff_time.py [--steps 50] [--configs c2,c3]
+prints one line per config: kernel ms (HIP events on the launch stream).
+"""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "go-mp3_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--configs", default="c2,c3")
+    a = ap.parse_args()
+    import torch
+    import mp3g
+    from concurrent.futures import ThreadPoolExecutor
+    from mp3g import synth
+    dev = torch.device("cuda:0")
+    st = torch.cuda.Stream(dev)
+    for cfg in a.configs.split(","):
+        ns, nf = (1, 10000) if cfg == "c2" else (1024, 1024)
+        with ThreadPoolExecutor(16) as ex:
+            datas = list(ex.map(lambda k: synth.encode_stream(1 + k, nf), range(ns)))
+        s = mp3g.scan_streams(datas, n_threads=16)
+        n = len(s["granules"])
+        d_g = torch.from_numpy(s["granules"].view(np.uint8).copy()).to(dev)
+        d_j = torch.from_numpy(s["jobs"].view(np.uint8).copy()).to(dev)
+        d_m = torch.from_numpy(s["main_data"].copy()).to(dev)
+        d_c = torch.empty(n * 1152, dtype=torch.int16, device=dev)
+        h = st.cuda_stream
+        for _ in range(5):
+            mp3g.huffman_execute(d_j, n, d_m, d_g, d_c, stream=h)
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(a.steps):
+            mp3g.huffman_execute(d_j, n, d_m, d_g, d_c, stream=h)
+        e1.record(st)
+        torch.cuda.synchronize(dev)
+        ms = e0.elapsed_time(e1) / a.steps
+        crc = int(d_c.view(torch.int32).sum().item()) & 0xffffffff
+        print(f"{os.environ.get('MP3G_LIB', 'default'):>28} {cfg} huffman_ms {ms:.4f} "
+              f"frames_per_s {n / 2 / ms * 1e3:.4g} coef_sum {crc:08x}", flush=True)
+        del d_g, d_j, d_m, d_c
+        time.sleep(0.1)
+
+
+if __name__ == "__main__":
+    main()
