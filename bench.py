@@ -181,7 +181,7 @@ def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle):
            # 2 x 1152 B coefficients + 2 x 63 B scale factors / count1 out per granule
            "huffman_algorithmic_bytes_per_launch": md + n * (96 + 2304 + 126),
            "huffman_algorithmic_gbps": round((md + n * (96 + 2304 + 126)) / (huff_ms * 1e-3) / 1e9, 2),
-           "huffman_traffic_bytes_per_launch": profiled_traffic(cfg, "mp3g::huff::huffman_kernel")[0],
+           "huffman_traffic_bytes_per_launch": profiled_traffic(cfg, "mp3g::huff::huffman_sorted_kernel")[0],
            "main_data_bytes": md, "bitstream_bytes": int(sum(len(d) for d in datas)),
            "host_scan_s": round(scan_s, 4), "host_scan_frames_per_s": round(frames / scan_s, 1),
            "host_scan_threads": 16, "writer_s": round(writer_s, 2),
@@ -204,7 +204,7 @@ def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle):
     return out
 
 
-PROFILE_TAG = "r02c"  # profiles/<tag>_<cfg>_<kernel>.json of the current kernels
+PROFILE_TAG = "r02d"  # profiles/<tag>_<cfg>_<kernel>.json of the current kernels
 
 
 def profiled_traffic(cfg, kernel):

@@ -16,15 +16,31 @@ import sys
 KERNEL = "granule"
 
 
-def counters(d, kernel=None):
+def counters(d, kernel=None, grid=None):
     kernel = kernel or KERNEL
     f = glob.glob(os.path.join(d, "*counter_collection.csv"))
     agg = collections.defaultdict(list)
     if f:
         for r in csv.DictReader(open(f[0])):
-            if kernel in r["Kernel_Name"]:
+            if kernel in r["Kernel_Name"] and (grid is None or int(r["Grid_Size"]) == grid):
                 agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in agg.items()}
+
+
+def full_launches(d, kernel):
+    """(grid, durations in ns) of the kernel's launches over the largest grid
+    in the kernel trace: the bench's timed launches.  A bench run also makes
+    smaller launches of the same kernel (the pipelined bitstream API decodes
+    groups of streams), which the rocprof stats average in."""
+    f = glob.glob(os.path.join(d, "*kernel_trace.csv"))
+    if not f:
+        return None, []
+    rows = [r for r in csv.DictReader(open(f[0])) if kernel in r["Kernel_Name"]]
+    if not rows:
+        return None, []
+    grid = max(int(r["Grid_Size_X"]) for r in rows)
+    return grid, [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows
+                  if int(r["Grid_Size_X"]) == grid]
 
 
 def main(src, tag, cfg, dst="profiles", bytes_per_launch=None, kernel=None, suffix=""):
@@ -32,12 +48,18 @@ def main(src, tag, cfg, dst="profiles", bytes_per_launch=None, kernel=None, suff
     base = os.path.join(src, f"prof_{tag}_{cfg}")
     stats = list(csv.DictReader(open(glob.glob(base + "_trace/*kernel_stats.csv")[0])))
     k = [r for r in stats if kernel in r["Name"]][0]
-    fetch = counters(base + "_fetch", kernel).get("FETCH_SIZE")
-    write = counters(base + "_write", kernel).get("WRITE_SIZE")
-    sq = counters(base + "_sq", kernel)
-    avg_ns = float(k["AverageNs"])
-    out = {"tag": tag, "config": cfg, "kernel": k["Name"].split("(")[0], "calls": int(k["Calls"]),
-           "avg_ns": avg_ns, "min_ns": float(k["MinNs"]), "max_ns": float(k["MaxNs"])}
+    grid, durs = full_launches(base + "_trace", kernel)
+    fetch = counters(base + "_fetch", kernel, grid).get("FETCH_SIZE")
+    write = counters(base + "_write", kernel, grid).get("WRITE_SIZE")
+    sq = counters(base + "_sq", kernel, grid)
+    out = {"tag": tag, "config": cfg, "kernel": k["Name"].split("(")[0],
+           "stats_calls": int(k["Calls"]), "stats_avg_ns": float(k["AverageNs"])}
+    if durs:  # the full-grid launches only (kernel trace)
+        avg_ns = sum(durs) / len(durs)
+        out.update(grid=grid, calls=len(durs), avg_ns=avg_ns, min_ns=min(durs), max_ns=max(durs))
+    else:
+        avg_ns = float(k["AverageNs"])
+        out.update(calls=int(k["Calls"]), avg_ns=avg_ns, min_ns=float(k["MinNs"]), max_ns=float(k["MaxNs"]))
     if fetch is not None and write is not None:
         hbm = (2 * fetch + write) * 1024
         out.update(fetch_kib=fetch, write_kib=write, hbm_bytes_per_launch_corrected=hbm,
