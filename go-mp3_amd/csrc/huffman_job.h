@@ -142,7 +142,9 @@ MP3G_HD_INLINE uint32_t decode_xy(Reader<kSwap>& r, const uint16_t* T, uint32_t 
 // pairs: huff_lut.h).  Far from the end (<= 19 + 2 * 14 = 47 bits to go)
 // every field comes out of one 64-bit peek; otherwise each read follows the
 // reference's clamping.
-template <bool kSwap>
+// kQuad = false: a big-values pair (c = d = 0 at compile time: no quad sign
+// work in the pair loop, c3 -1 %); kQuad = true: a count1 quad (lb = 0).
+template <bool kSwap, bool kQuad>
 MP3G_HD_INLINE void decode_sym(Reader<kSwap>& r, const uint16_t* T, uint32_t root, uint32_t lb, int& ao, int& bo,
                                int& co, int& dox) {
   r.refill();
@@ -153,8 +155,8 @@ MP3G_HD_INLINE void decode_sym(Reader<kSwap>& r, const uint16_t* T, uint32_t roo
     const uint32_t e = lut_leaf(T, root, (uint32_t)(p64 >> 32), &len);
     a = (int)((e >> 4) & 15u);
     b = (int)(e & 15u);
-    c = (int)((e >> 13) & 1u);
-    d = (int)((e >> 14) & 1u);
+    c = kQuad ? (int)((e >> 13) & 1u) : 0;
+    d = kQuad ? (int)((e >> 14) & 1u) : 0;
     uint32_t q = (uint32_t)((p64 << len) >> 32);  // the <= 28 bits after the codeword
     uint32_t o = len;
     // a: linbits of a 15, then the sign of a non-zero value; the same for b
@@ -184,8 +186,8 @@ MP3G_HD_INLINE void decode_sym(Reader<kSwap>& r, const uint16_t* T, uint32_t roo
     const uint32_t e = decode_xy(r, T, root);
     a = (int)((e >> 4) & 15u);
     b = (int)(e & 15u);
-    c = (int)((e >> 13) & 1u);
-    d = (int)((e >> 14) & 1u);
+    c = kQuad ? (int)((e >> 13) & 1u) : 0;
+    d = kQuad ? (int)((e >> 14) & 1u) : 0;
     if (lb && a == 15) a += (int)r.bits((int)lb);
     if (a && r.bit()) a = -a;
     if (lb && b == 15) b += (int)r.bits((int)lb);
@@ -403,7 +405,7 @@ MP3G_HD_INLINE int decode_job(const mp3g_hjob& job, uint64_t j, const uint64_t* 
           const uint32_t root = ii < r1 ? root0 : ii < r2 ? root1 : root2;
           const uint32_t lb = ii < r1 ? lb0 : ii < r2 ? lb1 : lb2;
           int a, b, c, d;
-          decode_sym(r, T, root, lb, a, b, c, d);
+          decode_sym<kSwap, false>(r, T, root, lb, a, b, c, d);
           w[sl] = (uint32_t)(uint16_t)(int16_t)a | ((uint32_t)(uint16_t)(int16_t)b << 16);
         }
       }
@@ -419,7 +421,7 @@ MP3G_HD_INLINE int decode_job(const mp3g_hjob& job, uint64_t j, const uint64_t* 
     i = bv2;
     while (i <= 572 && r.pos <= pend) {
       int a, b, c, d;
-      decode_sym(r, T, qroot, 0u, a, b, c, d);
+      decode_sym<kSwap, true>(r, T, qroot, 0u, a, b, c, d);
       out.put(i, a, b);
       out.put(i + 2, c, d);
       i += 4;
