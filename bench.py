@@ -170,6 +170,20 @@ def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle):
     assert n_p == n and all(x == 7 for x in st_p)
     pipe_s = pipe[-1]
     mp3g.lib().mp3g_release_cached_buffers()
+    # the io.Reader drop-in (mp3.NewDecoder + Read, decode.go:70-80, 361-388)
+    # on the first stream: read-ahead batches (host scan, then the Huffman and
+    # DSP kernels with the state carried between batches), 1 MiB reads
+    t = time.perf_counter()
+    dec = mp3g.Decoder(datas[0], mode=mode, device=idx)
+    got_bytes = 0
+    while True:
+        st_r, b = dec.read(1 << 20)
+        got_bytes += len(b)
+        if st_r != 0:
+            break
+    dec.close()
+    dec_s = time.perf_counter() - t
+    dec_frames = got_bytes // 4608
     frames = n // 2
     md = int(s["main_data"].nbytes)
     out = {"workload": f"{cfg} as Layer III bitstreams: {n_streams} x {n_frames} frames, 44.1 kHz stereo "
@@ -192,11 +206,17 @@ def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle):
                           "api": "mp3g_decode_streams_into (16 host threads, pinned PCM out)",
                           "serial_frames_per_s": round(frames / (scan_s + pcie_s), 1),
                           "host_scan_s": round(scan_s, 4), "h2d_huffman_dsp_d2h_s": round(pcie_s, 4),
-                          "pcm_d2h_bytes": int(n * 2304)}}
+                          "pcm_d2h_bytes": int(n * 2304)},
+           "decoder_api": {"frames_per_s": round(dec_frames / dec_s, 1), "frames": int(dec_frames),
+                           "api": "mp3g_decoder_new + mp3g_decoder_read (1 MiB reads), one stream",
+                           "read_status": int(st_r)}}
     if check_oracle:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import oracle  # parity check of the timed output (checker only)
+        t = time.perf_counter()
         ost, opcm = oracle.decode_all(datas[0])
+        out["cpu_full_decode"] = {"frames_per_s": round(n_frames / (time.perf_counter() - t), 1), "cores": 1,
+                                  "sample": "the same first stream, oracle NewDecoder + ReadAll (parse + DSP)"}
         got = d_p.cpu().numpy()[:len(opcm) // 2]
         want = np.frombuffer(opcm, np.int16)
         out["max_dpcm_lsb_vs_oracle"] = int(np.abs(got.astype(np.int32) - want).max()) if ost == 0 and \
@@ -364,6 +384,17 @@ def main():
                                    "sample": f"full c2 stream ({frames_rank} frames), oracle C "
                                              f"restatement -O2 -ffp-contract=off, 1 thread, median "
                                              f"of {args.cpu_repeats}"}
+            # all host cores of this rank's share (16 on the GPU box): the c2
+            # stream's granules as 16 independent streams, one per thread
+            reps = 16
+            gm, cm = np.concatenate([g] * reps), np.concatenate([c] * reps)
+            sm = mp3g.streams_for([len(g)] * reps)
+            t = time.perf_counter()
+            oracle.dsp_streams_mt(gm, cm, sm, reps)
+            out["cpu_baseline_all_cores"] = {
+                "value": round(frames_rank * reps / (time.perf_counter() - t), 1), "unit": "frames/s",
+                "cores": reps, "kind": "port",
+                "sample": f"{reps} copies of the c2 stream, one per thread (oracle, -O2 -ffp-contract=off)"}
             for m, r in res.items():
                 d = int(np.abs(r["pcm"].astype(np.int32) - ref.astype(np.int32)).max())
                 out["modes"][m]["max_dpcm_lsb"] = d
@@ -393,6 +424,23 @@ def main():
                 "host_parse_threads": 16,
                 "h2d_decode_d2h_s": round(xfer_s, 4), "host_parse_s": round(cfg_info["host_parse_s"], 4),
                 "note": "serial sum of the host parse (mp3g_parse_streams) and the PCIe-inclusive device leg"}
+            # the same bitstreams through the pipelined product call (host scan
+            # overlapping the GPU Huffman + DSP of the previous group of
+            # streams, PCM into pinned memory); the second call's time
+            gold = os.path.join(REPO, "tests", "golden")
+            datas = [open(os.path.join(gold, f), "rb").read() for f in ("classic_lame.mp3", "mpeg2.mp3")]
+            datas = datas * args.c5_copies
+            mode = mp3g.MODE_FAST if args.mode == "fast" else mp3g.MODE_EXACT
+            pipe = []
+            for _ in range(2):
+                t = time.perf_counter()
+                n_p, _, st_p = mp3g.decode_streams_into(datas, hp, mode=mode, n_threads=16, device=local)
+                pipe.append(time.perf_counter() - t)
+            mp3g.lib().mp3g_release_cached_buffers()
+            assert n_p == n_gran and all(x == 7 for x in st_p)
+            out["end_to_end"]["pipelined"] = {
+                "frames_per_s": round(frames_rank / pipe[-1], 1), "s": round(pipe[-1], 4),
+                "api": "mp3g_decode_streams_into (host scan + GPU Huffman + DSP, 16 host threads, pinned PCM out)"}
             sys.path.insert(0, os.path.join(REPO, "oracle"))
             import oracle  # parity check of the timed output (checker only)
             ref = oracle.dsp_streams_mt(g, c, streams, 16)
