@@ -173,12 +173,13 @@ def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle):
     # the io.Reader drop-in (mp3.NewDecoder + Read, decode.go:70-80, 361-388)
     # on the first stream: read-ahead batches (host scan, then the Huffman and
     # DSP kernels with the state carried between batches), 1 MiB reads
+    rbuf = np.empty(1 << 20, np.uint8)
     t = time.perf_counter()
     dec = mp3g.Decoder(datas[0], mode=mode, device=idx)
     got_bytes = 0
     while True:
-        st_r, b = dec.read(1 << 20)
-        got_bytes += len(b)
+        st_r, k = dec.read_full(rbuf)  # io.ReadFull: Read until 1 MiB (Read gives <= 1 frame)
+        got_bytes += k
         if st_r != 0:
             break
     dec.close()
@@ -208,7 +209,7 @@ def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle):
                           "host_scan_s": round(scan_s, 4), "h2d_huffman_dsp_d2h_s": round(pcie_s, 4),
                           "pcm_d2h_bytes": int(n * 2304)},
            "decoder_api": {"frames_per_s": round(dec_frames / dec_s, 1), "frames": int(dec_frames),
-                           "api": "mp3g_decoder_new + mp3g_decoder_read (1 MiB reads), one stream",
+                           "api": "mp3g_decoder_new + mp3g_decoder_read_full (io.ReadFull of 1 MiB), one stream",
                            "read_status": int(st_r)}}
     if check_oracle:
         sys.path.insert(0, os.path.join(REPO, "oracle"))

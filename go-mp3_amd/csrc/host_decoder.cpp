@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <thread>
@@ -61,6 +62,46 @@ St parse_all(const uint8_t* data, size_t len, std::vector<mp3g_granule>* g, std:
 
 }  // namespace
 
+// PCM read-ahead bytes in page-locked memory: the batch's PCM is copied from
+// the device straight into it (no pageable bounce, no second host copy).
+struct PinnedBytes {
+  uint8_t* p = nullptr;
+  size_t n = 0, cap = 0;
+  bool pinned = false;
+  PinnedBytes() = default;
+  PinnedBytes(const PinnedBytes&) = delete;
+  PinnedBytes& operator=(const PinnedBytes&) = delete;
+  ~PinnedBytes() { release(); }
+  void release() {
+    if (p) {
+      if (pinned) (void)hipHostFree(p);
+      else std::free(p);
+    }
+    p = nullptr;
+    n = cap = 0;
+  }
+  size_t size() const { return n; }
+  const uint8_t* data() const { return p; }
+  void clear() { n = 0; }
+  // room for `more` bytes past n (contents kept)
+  bool reserve_more(size_t more) {
+    if (n + more <= cap) return true;
+    const size_t c = std::max(n + more, 2 * cap);
+    void* q = nullptr;
+    bool pin = hipHostMalloc(&q, c, hipHostMallocDefault) == hipSuccess;
+    if (!pin) q = std::malloc(c);
+    if (!q) return false;
+    if (n) std::memcpy(q, p, n);
+    const size_t keep = n;
+    release();
+    p = static_cast<uint8_t*>(q);
+    n = keep;
+    cap = c;
+    pinned = pin;
+    return true;
+  }
+};
+
 // ---------------------------------------------------------------------------
 struct mp3g_decoder {
   std::vector<uint8_t> data;  // own copy: no caller pointer is retained
@@ -76,7 +117,7 @@ struct mp3g_decoder {
   std::vector<int64_t> frame_starts;
   int64_t pos = 0;
   // PCM read-ahead buffer
-  std::vector<uint8_t> buf;
+  PinnedBytes buf;
   size_t buf_off = 0;
   int pending = MP3G_OK;  // parse error to report once buf runs dry
   bool fresh = true;      // next batch starts from zero DSP state (frame = nil)
@@ -94,7 +135,10 @@ struct mp3g_decoder {
   std::vector<mp3g_granule> h_gran;
   std::vector<int16_t> h_coef;
   std::vector<mp3g_hjob> h_jobs;
-  std::vector<int16_t> h_pcm;
+  // the last plan (batches of the same length and state flags reuse it)
+  mp3g_plan* plan = nullptr;
+  uint64_t plan_n = 0;
+  uint32_t plan_flags = 0;
   std::vector<uint32_t> frame_pcm_bytes;  // PCM bytes of each frame of the last batch
   std::vector<int64_t> frame_src;         // source position after each frame of the last batch
   std::vector<size_t> frame_ends;         // end offset in buf of each buffered frame
@@ -108,6 +152,8 @@ struct mp3g_decoder {
     int prev = -1;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(device);
+    if (plan) mp3g_plan_destroy(plan);
+    buf.release();
     for (void* p : {(void*)d_gran, (void*)d_coef, (void*)d_pcm, (void*)d_state, (void*)d_jobs, (void*)d_md})
       if (p) (void)hipFree(p);
     if (stream) (void)hipStreamDestroy(stream);
@@ -210,9 +256,16 @@ struct mp3g_decoder {
     int rc = ensure_capacity(n);
     if (rc) return rc;
     mp3g_stream s{0, (uint32_t)n, (fresh ? 0u : (uint32_t)MP3G_STREAM_STATE_IN) | MP3G_STREAM_STATE_OUT};
-    mp3g_plan* plan = nullptr;
-    rc = mp3g_plan_create(device, &s, 1, 0, mode & ~(uint32_t)MP3G_FLAG_HOST_HUFFMAN, &plan);
-    if (rc) return rc;
+    if (!plan || plan_n != n || plan_flags != s.flags) {
+      if (plan) mp3g_plan_destroy(plan);
+      plan = nullptr;
+      rc = mp3g_plan_create(device, &s, 1, 0, mode & ~(uint32_t)MP3G_FLAG_HOST_HUFFMAN, &plan);
+      if (rc) return rc;
+      plan_n = n;
+      plan_flags = s.flags;
+    }
+    const size_t pcm_bytes = n * MP3G_PCM_BYTES_PER_GRANULE;
+    if (!buf.reserve_more(pcm_bytes)) return abi_fail(MP3G_ERR_OUT_OF_MEMORY, "decoder PCM buffer");
     hipError_t e = hipMemcpyAsync(d_gran, h_gran.data(), n * sizeof(mp3g_granule), hipMemcpyHostToDevice, stream);
     if (gpu_huffman()) {
       // main data + jobs up, then scale factors / Huffman codes on the device
@@ -229,31 +282,22 @@ struct mp3g_decoder {
         e = hipMemcpyAsync(d_jobs, h_jobs.data(), h_jobs.size() * sizeof(mp3g_hjob), hipMemcpyHostToDevice, stream);
       if (e == hipSuccess) {
         rc = mp3g_huffman_execute(device, d_jobs, n, d_md, d_gran, d_coef, stream);
-        if (rc) {
-          mp3g_plan_destroy(plan);
-          return rc;
-        }
+        if (rc) return rc;
       }
     } else if (e == hipSuccess) {
       e = hipMemcpyAsync(d_coef, h_coef.data(), h_coef.size() * sizeof(int16_t), hipMemcpyHostToDevice, stream);
     }
-    if (e != hipSuccess) {
-      mp3g_plan_destroy(plan);
-      return abi_fail(MP3G_ERR_DEVICE, "decoder H2D copy");
-    }
+    if (e != hipSuccess) return abi_fail(MP3G_ERR_DEVICE, "decoder H2D copy");
     rc = mp3g_plan_execute(plan, d_gran, d_coef, d_state, d_state + 1, d_pcm, stream);
-    mp3g_plan_destroy(plan);
     if (rc) return rc;
-    h_pcm.resize(n * MP3G_COEF_PER_GRANULE);
-    e = hipMemcpyAsync(h_pcm.data(), d_pcm, n * MP3G_PCM_BYTES_PER_GRANULE, hipMemcpyDeviceToHost, stream);
+    e = hipMemcpyAsync(buf.p + buf.n, d_pcm, pcm_bytes, hipMemcpyDeviceToHost, stream);
     // carry: out -> in for the next batch
     if (e == hipSuccess) e = hipMemcpyAsync(d_state, d_state + 1, sizeof(mp3g_state), hipMemcpyDeviceToDevice, stream);
     if (e == hipSuccess) e = hipStreamSynchronize(stream);
     if (e != hipSuccess) return abi_fail(MP3G_ERR_DEVICE, "decoder batch");
     fresh = false;
-    const uint8_t* p = reinterpret_cast<const uint8_t*>(h_pcm.data());
-    buf.insert(buf.end(), p, p + n * MP3G_PCM_BYTES_PER_GRANULE);
-    size_t end = buf.size() - n * MP3G_PCM_BYTES_PER_GRANULE;
+    size_t end = buf.n;
+    buf.n += pcm_bytes;
     for (uint32_t b : frame_pcm_bytes) frame_ends.push_back(end += b);
     frame_src_ends.insert(frame_src_ends.end(), frame_src.begin(), frame_src.end());
     return MP3G_OK;
@@ -440,6 +484,18 @@ int mp3g_decoder_read(mp3g_decoder* d, uint8_t* out, size_t cap, size_t* n) {  /
   d->buf_off += k;
   d->pos += (int64_t)k;
   *n = k;
+  return MP3G_OK;
+}
+
+int mp3g_decoder_read_full(mp3g_decoder* d, uint8_t* out, size_t cap, size_t* n) {  // io.ReadFull
+  if (!d || !n || (cap && !out)) return abi_fail(MP3G_ERR_INVALID_ARGUMENT, "null argument");
+  *n = 0;
+  while (*n < cap) {
+    size_t k = 0;
+    const int rc = mp3g_decoder_read(d, out + *n, cap - *n, &k);
+    *n += k;
+    if (rc != MP3G_OK) return rc;
+  }
   return MP3G_OK;
 }
 

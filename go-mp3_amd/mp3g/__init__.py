@@ -108,6 +108,7 @@ def lib():
         L.mp3g_decoder_new.argtypes = [vp, sz, C.c_int, C.c_int, u32, C.POINTER(vp)]
         L.mp3g_decoder_free.argtypes = [vp]
         L.mp3g_decoder_read.argtypes = [vp, vp, sz, C.POINTER(sz)]
+        L.mp3g_decoder_read_full.argtypes = [vp, vp, sz, C.POINTER(sz)]
         L.mp3g_decoder_seek.argtypes = [vp, i64, C.c_int, C.POINTER(i64)]
         L.mp3g_decoder_info.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(i64), C.POINTER(i64),
                                         C.POINTER(i64)]
@@ -411,6 +412,17 @@ class Decoder:
         k = C.c_size_t()
         st = lib().mp3g_decoder_read(self._h, _ptr(out), n, C.byref(k))
         return st, out[:k.value].tobytes()
+
+    def read_full(self, out):
+        """io.ReadFull into a writable buffer (numpy uint8/int16 array or a
+        pinned torch tensor): (status, bytes delivered)."""
+        if hasattr(out, "data_ptr"):
+            ptr, cap = out.data_ptr(), out.numel() * out.element_size()
+        else:
+            ptr, cap = out.ctypes.data, out.nbytes
+        k = C.c_size_t()
+        st = lib().mp3g_decoder_read_full(self._h, C.c_void_p(ptr), cap, C.byref(k))
+        return st, k.value
 
     def read_all(self):
         chunks = []

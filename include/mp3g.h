@@ -301,6 +301,11 @@ int mp3g_decoder_new(const uint8_t* data, size_t len, int seekable, int device, 
                      mp3g_decoder** out);
 void mp3g_decoder_free(mp3g_decoder* dec);
 int mp3g_decoder_read(mp3g_decoder* dec, uint8_t* buf, size_t cap, size_t* n);
+/* io.ReadFull over Decoder.Read (Go's io.ReadFull loops Read the same way):
+ * repeated reads until `cap` bytes, EOF or an error.  Returns MP3G_OK with
+ * *n == cap, or the status that ended it (MP3G_EOF / the frame's error) with
+ * *n = the bytes delivered before it.  One call instead of one per frame. */
+int mp3g_decoder_read_full(mp3g_decoder* dec, uint8_t* buf, size_t cap, size_t* n);
 /* whence: 0 = io.SeekStart, 1 = io.SeekCurrent, 2 = io.SeekEnd */
 int mp3g_decoder_seek(mp3g_decoder* dec, int64_t offset, int whence, int64_t* newpos);
 /* SampleRate, Length (-1 if unknown), BytesPerFrame, current position (bytes) */

@@ -46,6 +46,26 @@ def test_read_all_exact(gpu, sample_files, golden, name, host_huffman):
 
 
 @pytest.mark.parametrize("name", ["classic_lame.mp3", "mpeg2.mp3"])
+@pytest.mark.parametrize("cap", [4608, 1 << 20, 50_000_000])
+def test_read_full(gpu, sample_files, name, cap):
+    """mp3g_decoder_read_full (io.ReadFull over Read): the same bytes as the
+    oracle's ReadAll, cap-sized pieces, EOF with the short tail."""
+    d, o = both(gpu, sample_files[name])
+    st2, want = o.read_all()
+    assert st2 == oracle.ORC_EOF
+    got = []
+    buf = np.zeros(cap, np.uint8)
+    while True:
+        st, k = d.read_full(buf)
+        got.append(buf[:k].tobytes())
+        if st != 0:
+            assert st == 7 and k < cap
+            break
+        assert k == cap
+    assert b"".join(got) == want
+
+
+@pytest.mark.parametrize("name", ["classic_lame.mp3", "mpeg2.mp3"])
 def test_read_all_fast(gpu, sample_files, name):
     d, o = both(gpu, sample_files[name], mode=gpu.MODE_FAST)
     b, b2 = read_all_both(d, o)
