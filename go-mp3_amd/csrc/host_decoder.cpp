@@ -102,6 +102,30 @@ struct PinnedBytes {
   }
 };
 
+// One read-ahead batch of frames as the host scan (or full parse) left it:
+// everything its device leg needs, so that the next batch can be scanned
+// while this one is on the device.
+struct Batch {
+  std::vector<mp3g_granule> gran;
+  std::vector<int16_t> coef;   // MP3G_FLAG_HOST_HUFFMAN
+  std::vector<mp3g_hjob> jobs;  // default: jobs into `md`
+  std::vector<uint8_t> md;      // the main data the jobs address (a snapshot)
+  std::vector<uint32_t> frame_pcm_bytes;  // PCM bytes of each frame
+  std::vector<int64_t> frame_src;         // source position after each frame
+  int err = MP3G_OK;  // status that ended the batch (EOF / parse error), after its frames
+  bool fresh = true;  // starts from zero DSP state (frame = nil)
+  size_t n() const { return gran.size(); }
+  void clear() {
+    gran.clear();
+    coef.clear();
+    jobs.clear();
+    md.clear();
+    frame_pcm_bytes.clear();
+    frame_src.clear();
+    err = MP3G_OK;
+  }
+};
+
 // ---------------------------------------------------------------------------
 struct mp3g_decoder {
   std::vector<uint8_t> data;  // own copy: no caller pointer is retained
@@ -116,12 +140,18 @@ struct mp3g_decoder {
   int64_t bytes_per_frame = 0;
   std::vector<int64_t> frame_starts;
   int64_t pos = 0;
-  // PCM read-ahead buffer
-  PinnedBytes buf;
+  // PCM being served (one batch) and the PCM of the batch on the device
+  PinnedBytes buf, ahead;
   size_t buf_off = 0;
   int pending = MP3G_OK;  // parse error to report once buf runs dry
-  bool fresh = true;      // next batch starts from zero DSP state (frame = nil)
+  bool scan_fresh = true;  // the next scanned batch starts from zero DSP state
   size_t batch_frames = 16;
+  // Read-ahead pipeline: bat[fl] is on the device (its PCM lands in `ahead`),
+  // bat[sc] is scanned and waits for the device; one slot each.
+  Batch bat[2];
+  bool inflight = false, scanned = false;
+  int fl = 0, sc = 1;
+  uint32_t first_header = 0;  // header of the first granule served (SampleRate)
   // device resources (grown on demand)
   hipStream_t stream = nullptr;
   mp3g_granule* d_gran = nullptr;
@@ -131,16 +161,10 @@ struct mp3g_decoder {
   mp3g_hjob* d_jobs = nullptr;
   uint8_t* d_md = nullptr;
   size_t cap_granules = 0, cap_md = 0;
-  // host staging
-  std::vector<mp3g_granule> h_gran;
-  std::vector<int16_t> h_coef;
-  std::vector<mp3g_hjob> h_jobs;
   // the last plan (batches of the same length and state flags reuse it)
   mp3g_plan* plan = nullptr;
   uint64_t plan_n = 0;
   uint32_t plan_flags = 0;
-  std::vector<uint32_t> frame_pcm_bytes;  // PCM bytes of each frame of the last batch
-  std::vector<int64_t> frame_src;         // source position after each frame of the last batch
   std::vector<size_t> frame_ends;         // end offset in buf of each buffered frame
   std::vector<int64_t> frame_src_ends;    // source position after each buffered frame
   // index into frame_ends of the frame the reference read last: Decoder.Read
@@ -152,8 +176,10 @@ struct mp3g_decoder {
     int prev = -1;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(device);
+    if (stream) (void)hipStreamSynchronize(stream);
     if (plan) mp3g_plan_destroy(plan);
     buf.release();
+    ahead.release();
     for (void* p : {(void*)d_gran, (void*)d_coef, (void*)d_pcm, (void*)d_state, (void*)d_jobs, (void*)d_md})
       if (p) (void)hipFree(p);
     if (stream) (void)hipStreamDestroy(stream);
@@ -176,17 +202,14 @@ struct mp3g_decoder {
     return MP3G_OK;
   }
 
-  // Parses up to `max_frames` frames and decodes them on the device,
-  // appending their PCM to buf.  Returns MP3G_OK if at least one frame was
-  // decoded (a later parse error is kept in `pending`), else the error.
   bool gpu_huffman() const { return (mode & MP3G_FLAG_HOST_HUFFMAN) == 0; }
 
-  int decode_batch(size_t max_frames) {
-    h_gran.clear();
-    h_coef.clear();
-    h_jobs.clear();
-    frame_pcm_bytes.clear();
-    frame_src.clear();
+  // Scans (or parses) up to `max_frames` frames into b.  A failing frame ends
+  // the batch: b.err, the reservoir is dropped and the next batch starts from
+  // zero DSP state (d.frame = nil after a failed frame.Read).
+  void scan_batch(Batch& b, size_t max_frames) {
+    b.clear();
+    b.fresh = scan_fresh;
     St st = St::kOk;
     if (gpu_huffman()) {
       // drop main data no later frame can reach (the reservoir is < 2 KB)
@@ -200,39 +223,31 @@ struct mp3g_decoder {
         st = scanner.next(src, &f, &md);
         if (st != St::kOk) break;
         for (int gr = 0; gr < f.n_granules; gr++) {
-          h_gran.push_back(f.gran[gr]);
-          h_jobs.push_back(f.job[gr][0]);
-          h_jobs.push_back(f.job[gr][1]);
+          b.gran.push_back(f.gran[gr]);
+          b.jobs.push_back(f.job[gr][0]);
+          b.jobs.push_back(f.job[gr][1]);
         }
-        frame_pcm_bytes.push_back((uint32_t)(f.n_granules * MP3G_PCM_BYTES_PER_GRANULE));
-        frame_src.push_back(src.pos);
+        b.frame_pcm_bytes.push_back((uint32_t)(f.n_granules * MP3G_PCM_BYTES_PER_GRANULE));
+        b.frame_src.push_back(src.pos);
       }
+      if (!b.gran.empty()) b.md.assign(md.begin(), md.end());  // the scanner keeps editing md
     } else {
       host::ParsedFrame f;
       for (size_t i = 0; i < max_frames; i++) {
         st = parser.next(src, &f);
         if (st != St::kOk) break;
         for (int gr = 0; gr < f.n_granules; gr++) {
-          h_gran.push_back(f.gran[gr]);
-          h_coef.insert(h_coef.end(), f.coef[gr], f.coef[gr] + MP3G_COEF_PER_GRANULE);
+          b.gran.push_back(f.gran[gr]);
+          b.coef.insert(b.coef.end(), f.coef[gr], f.coef[gr] + MP3G_COEF_PER_GRANULE);
         }
-        frame_pcm_bytes.push_back((uint32_t)(f.n_granules * MP3G_PCM_BYTES_PER_GRANULE));
-        frame_src.push_back(src.pos);
+        b.frame_pcm_bytes.push_back((uint32_t)(f.n_granules * MP3G_PCM_BYTES_PER_GRANULE));
+        b.frame_src.push_back(src.pos);
       }
     }
-    const int err = st == St::kOk ? MP3G_OK : to_status(st);
-    if (err != MP3G_OK) reset_reservoir();  // d.frame = nil after a failed frame.Read
-    if (h_gran.empty()) {
-      fresh = true;
-      return err;
-    }
-    int rc = run_device();
-    if (rc != MP3G_OK) return rc;
-    if (err != MP3G_OK) {
-      pending = err;
-      fresh = true;  // the frame after a failed one starts from zero state
-    }
-    return MP3G_OK;
+    b.err = st == St::kOk ? MP3G_OK : to_status(st);
+    if (b.err != MP3G_OK) reset_reservoir();
+    scan_fresh = b.gran.empty() || b.err != MP3G_OK;
+    batch_frames = std::min<size_t>(batch_frames * 2, 1024);
   }
 
   void reset_reservoir() {
@@ -240,8 +255,10 @@ struct mp3g_decoder {
     scanner.reset();
   }
 
-  int run_device() {
-    const size_t n = h_gran.size();
+  // Enqueues batch b (n() > 0) on the decoder's stream: H2D, Huffman kernel,
+  // DSP plan (state carried on the device), PCM D2H into `ahead`.
+  int submit(const Batch& b) {
+    const size_t n = b.n();
     int prev = -1;
     (void)hipGetDevice(&prev);
     if (hipSetDevice(device) != hipSuccess) return abi_fail(MP3G_ERR_NO_DEVICE, "hipSetDevice");
@@ -255,7 +272,7 @@ struct mp3g_decoder {
       return abi_fail(MP3G_ERR_OUT_OF_MEMORY, "decoder state");
     int rc = ensure_capacity(n);
     if (rc) return rc;
-    mp3g_stream s{0, (uint32_t)n, (fresh ? 0u : (uint32_t)MP3G_STREAM_STATE_IN) | MP3G_STREAM_STATE_OUT};
+    mp3g_stream s{0, (uint32_t)n, (b.fresh ? 0u : (uint32_t)MP3G_STREAM_STATE_IN) | MP3G_STREAM_STATE_OUT};
     if (!plan || plan_n != n || plan_flags != s.flags) {
       if (plan) mp3g_plan_destroy(plan);
       plan = nullptr;
@@ -265,11 +282,12 @@ struct mp3g_decoder {
       plan_flags = s.flags;
     }
     const size_t pcm_bytes = n * MP3G_PCM_BYTES_PER_GRANULE;
-    if (!buf.reserve_more(pcm_bytes)) return abi_fail(MP3G_ERR_OUT_OF_MEMORY, "decoder PCM buffer");
-    hipError_t e = hipMemcpyAsync(d_gran, h_gran.data(), n * sizeof(mp3g_granule), hipMemcpyHostToDevice, stream);
+    ahead.clear();
+    if (!ahead.reserve_more(pcm_bytes)) return abi_fail(MP3G_ERR_OUT_OF_MEMORY, "decoder PCM buffer");
+    hipError_t e = hipMemcpyAsync(d_gran, b.gran.data(), n * sizeof(mp3g_granule), hipMemcpyHostToDevice, stream);
     if (gpu_huffman()) {
       // main data + jobs up, then scale factors / Huffman codes on the device
-      const size_t mdb = md.size() + 16;  // + padding for the 32-bit window loads
+      const size_t mdb = b.md.size() + 16;  // + padding for the 32-bit window loads
       if (e == hipSuccess && mdb > cap_md) {
         if (d_md) (void)hipFree(d_md);
         d_md = nullptr;
@@ -277,30 +295,46 @@ struct mp3g_decoder {
         e = hipMalloc(&d_md, cap_md);
         if (e != hipSuccess) cap_md = 0;
       }
-      if (e == hipSuccess && !md.empty()) e = hipMemcpyAsync(d_md, md.data(), md.size(), hipMemcpyHostToDevice, stream);
+      if (e == hipSuccess && !b.md.empty())
+        e = hipMemcpyAsync(d_md, b.md.data(), b.md.size(), hipMemcpyHostToDevice, stream);
       if (e == hipSuccess)
-        e = hipMemcpyAsync(d_jobs, h_jobs.data(), h_jobs.size() * sizeof(mp3g_hjob), hipMemcpyHostToDevice, stream);
+        e = hipMemcpyAsync(d_jobs, b.jobs.data(), b.jobs.size() * sizeof(mp3g_hjob), hipMemcpyHostToDevice, stream);
       if (e == hipSuccess) {
         rc = mp3g_huffman_execute(device, d_jobs, n, d_md, d_gran, d_coef, stream);
         if (rc) return rc;
       }
     } else if (e == hipSuccess) {
-      e = hipMemcpyAsync(d_coef, h_coef.data(), h_coef.size() * sizeof(int16_t), hipMemcpyHostToDevice, stream);
+      e = hipMemcpyAsync(d_coef, b.coef.data(), b.coef.size() * sizeof(int16_t), hipMemcpyHostToDevice, stream);
     }
     if (e != hipSuccess) return abi_fail(MP3G_ERR_DEVICE, "decoder H2D copy");
     rc = mp3g_plan_execute(plan, d_gran, d_coef, d_state, d_state + 1, d_pcm, stream);
     if (rc) return rc;
-    e = hipMemcpyAsync(buf.p + buf.n, d_pcm, pcm_bytes, hipMemcpyDeviceToHost, stream);
+    e = hipMemcpyAsync(ahead.p, d_pcm, pcm_bytes, hipMemcpyDeviceToHost, stream);
     // carry: out -> in for the next batch
     if (e == hipSuccess) e = hipMemcpyAsync(d_state, d_state + 1, sizeof(mp3g_state), hipMemcpyDeviceToDevice, stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(stream);
     if (e != hipSuccess) return abi_fail(MP3G_ERR_DEVICE, "decoder batch");
-    fresh = false;
-    size_t end = buf.n;
-    buf.n += pcm_bytes;
-    for (uint32_t b : frame_pcm_bytes) frame_ends.push_back(end += b);
-    frame_src_ends.insert(frame_src_ends.end(), frame_src.begin(), frame_src.end());
+    ahead.n = pcm_bytes;
     return MP3G_OK;
+  }
+
+  // Waits for the batch on the device and makes it the served buffer.
+  int complete(const Batch& b) {
+    if (hipStreamSynchronize(stream) != hipSuccess) return abi_fail(MP3G_ERR_DEVICE, "decoder batch");
+    std::swap(buf.p, ahead.p);
+    std::swap(buf.n, ahead.n);
+    std::swap(buf.cap, ahead.cap);
+    std::swap(buf.pinned, ahead.pinned);
+    size_t end = 0;
+    for (uint32_t x : b.frame_pcm_bytes) frame_ends.push_back(end += x);
+    frame_src_ends.insert(frame_src_ends.end(), b.frame_src.begin(), b.frame_src.end());
+    if (!first_header) first_header = b.gran.front().header;
+    return MP3G_OK;
+  }
+
+  // Drops the read-ahead (seek): waits for the device, forgets both slots.
+  void cancel_read_ahead() {
+    if (inflight && stream) (void)hipStreamSynchronize(stream);
+    inflight = scanned = false;
   }
 
   void buf_reset() {
@@ -319,7 +353,13 @@ struct mp3g_decoder {
     if (next_end < frame_src_ends.size()) src.seek(frame_src_ends[next_end], 0, nullptr);
   }
 
-  // readFrame for Read: decode the next batch (read-ahead grows to 1024 frames)
+  // readFrame for Read: serve the next batch (read-ahead grows to 1024
+  // frames).  Pipelined: the batch served now was put on the device by the
+  // previous refill; the next scanned batch goes on the device and the one
+  // after it is scanned on the host while the device works.  A batch that
+  // ends in an error (or EOF) is the last one read ahead; its status is
+  // returned once its PCM has been read, and the refill after that resumes
+  // scanning where the failed frame left the source.
   int refill() {
     if (pending != MP3G_OK) {
       const int e = pending;
@@ -328,9 +368,47 @@ struct mp3g_decoder {
       return e;
     }
     buf_reset();
-    const int rc = decode_batch(batch_frames);
-    batch_frames = std::min<size_t>(batch_frames * 2, 1024);
-    return rc;
+    int served;
+    if (inflight) {
+      served = fl;
+      inflight = false;
+    } else {
+      served = scanned ? sc : fl;
+      if (!scanned) scan_batch(bat[served], batch_frames);
+      scanned = false;
+      Batch& b = bat[served];
+      if (b.n() == 0) return b.err == MP3G_OK ? MP3G_EOF : b.err;
+      const int rc = submit(b);
+      if (rc) return rc;
+    }
+    Batch& b = bat[served];
+    int rc = complete(b);
+    if (rc) return rc;
+    if (b.err != MP3G_OK) {
+      pending = b.err;
+      return MP3G_OK;
+    }
+    // read ahead: the scanned batch (or a fresh scan) goes on the device...
+    const int other = served ^ 1;
+    if (!scanned) scan_batch(bat[other], batch_frames);
+    scanned = false;
+    Batch& nb = bat[other];
+    if (nb.n() == 0) {
+      scanned = true;  // only a status: returned by the refill that would serve it
+      sc = other;
+      return MP3G_OK;
+    }
+    rc = submit(nb);
+    if (rc) return rc;
+    inflight = true;
+    fl = other;
+    // ...and the one after it is scanned while the device decodes
+    if (nb.err == MP3G_OK) {
+      scan_batch(bat[served], batch_frames);
+      scanned = true;
+      sc = served;
+    }
+    return MP3G_OK;
   }
 
   // ensureFrameStartsAndLength (decode.go:154-216)
@@ -450,12 +528,9 @@ int mp3g_decoder_new(const uint8_t* data, size_t len, int seekable, int device, 
   // NewDecoder (decode.go:361-388): skip tags, read (here: read ahead from)
   // the first frame, take the sample rate, scan frame starts + length
   int rc = to_status(d->src.skip_tags());
+  if (rc == MP3G_OK) rc = d->refill();
   if (rc == MP3G_OK) {
-    d->buf_reset();
-    rc = d->decode_batch(d->batch_frames);
-  }
-  if (rc == MP3G_OK) {
-    d->sample_rate = host::header_sample_rate(d->h_gran.front().header);
+    d->sample_rate = host::header_sample_rate(d->first_header);
     rc = d->ensure_length();
   }
   if (rc != MP3G_OK) {
@@ -513,11 +588,12 @@ int mp3g_decoder_seek(mp3g_decoder* d, int64_t offset, int whence, int64_t* newp
     default: return abi_fail(MP3G_ERR_INVALID_ARGUMENT, "mp3: invalid whence");
   }
   d->pos = npos;
+  d->cancel_read_ahead();
   d->rewind_read_ahead();
   d->buf_reset();
   d->reset_reservoir();  // d.frame = nil
   d->md.clear();
-  d->fresh = true;
+  d->scan_fresh = true;
   d->pending = MP3G_OK;
   d->batch_frames = 16;
   if (d->pos < 0) d->pos = 0;
@@ -535,15 +611,14 @@ int mp3g_decoder_seek(mp3g_decoder* d, int64_t offset, int whence, int64_t* newp
   if (f >= (int64_t)d->frame_starts.size())
     return abi_fail(MP3G_ERR_UNSUPPORTED, "frame index out of range (the reference panics)");
   if (!d->src.seek(d->frame_starts[f], 0, nullptr)) return abi_fail(MP3G_ERR_PARSE, "seek");
-  int rc = d->decode_batch(d->batch_frames);
+  int rc = d->refill();
   if (rc != MP3G_OK) return rc;
-  if ((int)d->frame_pcm_bytes.size() < need) {  // the reference's 2nd readFrame failed
+  if ((int)d->frame_ends.size() < need) {  // the reference's 2nd readFrame failed
     rc = d->pending;
     d->pending = MP3G_OK;
     return rc;
   }
-  size_t ref_len = 0;  // the reference's d.buf holds exactly `need` frames here
-  for (int i = 0; i < need; i++) ref_len += d->frame_pcm_bytes[i];
+  const size_t ref_len = d->frame_ends[need - 1];  // the reference's d.buf holds exactly `need` frames here
   const int64_t off = need == 2 ? d->bytes_per_frame + d->pos % d->bytes_per_frame : d->pos;
   if (off > (int64_t)ref_len) return abi_fail(MP3G_ERR_UNSUPPORTED, "slice out of range (the reference panics)");
   d->buf_off = (size_t)off;
