@@ -225,7 +225,7 @@ def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle):
     return out
 
 
-PROFILE_TAG = "r02d"  # profiles/<tag>_<cfg>_<kernel>.json of the current kernels
+PROFILE_TAG = "r02e"  # profiles/<tag>_<cfg>_<kernel>.json of the current kernels
 
 
 def profiled_traffic(cfg, kernel):
