@@ -102,6 +102,13 @@ struct PinnedBytes {
   }
 };
 
+// Read-ahead batches start at 16 frames and double up to this.  A small
+// batch is latency-bound on the device (the main-data kernel's lanes each walk
+// one granule-channel's Huffman codes: ~0.2 ms for any batch that fits one
+// round of waves), so the cap is set by that, not by the host scan (~0.2 us
+// per frame): 8,192 frames = 32,768 jobs is still one round.
+constexpr size_t kMaxBatchFrames = 8192;
+
 // One read-ahead batch of frames as the host scan (or full parse) left it:
 // everything its device leg needs, so that the next batch can be scanned
 // while this one is on the device.
@@ -247,7 +254,7 @@ struct mp3g_decoder {
     b.err = st == St::kOk ? MP3G_OK : to_status(st);
     if (b.err != MP3G_OK) reset_reservoir();
     scan_fresh = b.gran.empty() || b.err != MP3G_OK;
-    batch_frames = std::min<size_t>(batch_frames * 2, 1024);
+    batch_frames = std::min<size_t>(batch_frames * 2, kMaxBatchFrames);
   }
 
   void reset_reservoir() {
@@ -353,8 +360,8 @@ struct mp3g_decoder {
     if (next_end < frame_src_ends.size()) src.seek(frame_src_ends[next_end], 0, nullptr);
   }
 
-  // readFrame for Read: serve the next batch (read-ahead grows to 1024
-  // frames).  Pipelined: the batch served now was put on the device by the
+  // readFrame for Read: serve the next batch (read-ahead grows to
+  // kMaxBatchFrames).  Pipelined: the batch served now was put on the device by the
   // previous refill; the next scanned batch goes on the device and the one
   // after it is scanned on the host while the device works.  A batch that
   // ends in an error (or EOF) is the last one read ahead; its status is

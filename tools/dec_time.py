@@ -12,7 +12,7 @@ sys.path.insert(0, os.path.join(ROOT, "go-mp3_amd"))
 import mp3g  # noqa: E402
 from mp3g import synth  # noqa: E402
 
-data = synth.encode_stream(1, 10000)
+data = synth.encode_stream(1, int(sys.argv[1]) if len(sys.argv) > 1 else 10000)
 rbuf = np.empty(1 << 20, np.uint8)
 for rep in range(3):
     for mode in (mp3g.MODE_FAST, mp3g.MODE_EXACT):
