@@ -55,6 +55,9 @@ def parse():
     ap.add_argument("--gather", action="store_true", help="also time an RCCL PCM gather to rank 0")
     ap.add_argument("--no-bitstream", action="store_true",
                     help="skip the bitstream leg (host scan + GPU Huffman + DSP on real Layer III streams)")
+    ap.add_argument("--no-pipelined", action="store_true",
+                    help="bitstream leg without the pipelined / io.Reader API runs (profiling: every "
+                         "kernel launch then has the timed launches' size)")
     return ap.parse_args()
 
 
@@ -90,7 +93,7 @@ def build_workload(cfg, rank, seed_base=1, c5_copies=256):
                                     "streams_per_gpu": 1024, "frames_per_stream": 1024}
 
 
-def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle):
+def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle, pipelined=True):
     """the same workload as real Layer III bitstreams
     (synthetic writer, go-mp3_amd/csrc/synth_enc.cpp): host scan (headers,
     side info, reservoir) on 16 threads, then on device-resident input the
@@ -163,26 +166,27 @@ def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle):
     # (the first call allocates its staging and device buffers, the second
     # reuses them: the time of the second)
     pipe = []
-    for _ in range(2):
+    for _ in range(2 if pipelined else 0):
         t = time.perf_counter()
         n_p, _, st_p = mp3g.decode_streams_into(datas, hp, mode=mode, n_threads=16, device=idx)
         pipe.append(time.perf_counter() - t)
-    assert n_p == n and all(x == 7 for x in st_p)
-    pipe_s = pipe[-1]
+        assert n_p == n and all(x == 7 for x in st_p)
+    pipe_s = pipe[-1] if pipe else float("nan")
     mp3g.lib().mp3g_release_cached_buffers()
     # the io.Reader drop-in (mp3.NewDecoder + Read, decode.go:70-80, 361-388)
     # on the first stream: read-ahead batches (host scan, then the Huffman and
     # DSP kernels with the state carried between batches), 1 MiB reads
     rbuf = np.empty(1 << 20, np.uint8)
     t = time.perf_counter()
-    dec = mp3g.Decoder(datas[0], mode=mode, device=idx)
-    got_bytes = 0
-    while True:
-        st_r, k = dec.read_full(rbuf)  # io.ReadFull: Read until 1 MiB (Read gives <= 1 frame)
-        got_bytes += k
-        if st_r != 0:
-            break
-    dec.close()
+    got_bytes, st_r = 0, None
+    if pipelined:
+        dec = mp3g.Decoder(datas[0], mode=mode, device=idx)
+        while True:
+            st_r, k = dec.read_full(rbuf)  # io.ReadFull: Read until 1 MiB (Read gives <= 1 frame)
+            got_bytes += k
+            if st_r != 0:
+                break
+        dec.close()
     dec_s = time.perf_counter() - t
     dec_frames = got_bytes // 4608
     frames = n // 2
@@ -203,12 +207,14 @@ def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle):
            # bitstream bytes in host memory -> PCM in host memory: the
            # pipelined product call (measured), and for reference the serial
            # sum of the host scan and the PCIe-inclusive device leg
-           "end_to_end": {"frames_per_s": round(frames / pipe_s, 1), "pipelined_s": round(pipe_s, 4),
+           "end_to_end": {"frames_per_s": round(frames / pipe_s, 1) if pipe else None,
+                          "pipelined_s": round(pipe_s, 4) if pipe else None,
                           "api": "mp3g_decode_streams_into (16 host threads, pinned PCM out)",
                           "serial_frames_per_s": round(frames / (scan_s + pcie_s), 1),
                           "host_scan_s": round(scan_s, 4), "h2d_huffman_dsp_d2h_s": round(pcie_s, 4),
                           "pcm_d2h_bytes": int(n * 2304)},
-           "decoder_api": {"frames_per_s": round(dec_frames / dec_s, 1), "frames": int(dec_frames),
+           "decoder_api": None if not pipelined else {
+                           "frames_per_s": round(dec_frames / dec_s, 1), "frames": int(dec_frames),
                            "api": "mp3g_decoder_new + mp3g_decoder_read_full (io.ReadFull of 1 MiB), one stream",
                            "read_status": int(st_r)}}
     if check_oracle:
@@ -322,7 +328,8 @@ def main():
     if not args.no_bitstream and args.config in ("c2", "c3"):
         bitstream = bitstream_leg(args.config, rank, dev, stream,
                                   mp3g.MODE_FAST if args.mode == "fast" else mp3g.MODE_EXACT,
-                                  args.steps, args.warmup, check_oracle=rank == 0 and args.config == "c2")
+                                  args.steps, args.warmup, check_oracle=rank == 0 and args.config == "c2",
+                                  pipelined=not args.no_pipelined)
 
     gather_ms = None
     if args.gather and world > 1:

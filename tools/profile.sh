@@ -24,7 +24,7 @@ run() {  # name timeout args...
 cfgs="c2 c3"; [ "$WHICH" != both ] && cfgs=$WHICH
 for cfg in $cfgs; do
   steps=20; [ $cfg = c3 ] && steps=5
-  B="bench.py --config $cfg --steps $steps --warmup 2 --no-cpu-baseline $EXTRA"
+  B="bench.py --config $cfg --steps $steps --warmup 2 --no-cpu-baseline --no-pipelined $EXTRA"
   run trace_$cfg 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_${TAG}_${cfg}_trace -o run -- python3 $B
   run fetch_$cfg 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/prof_${TAG}_${cfg}_fetch -o run -- python3 $B
   run write_$cfg 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/prof_${TAG}_${cfg}_write -o run -- python3 $B
