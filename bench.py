@@ -231,7 +231,7 @@ def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle, pip
     return out
 
 
-PROFILE_TAG = "r02e"  # profiles/<tag>_<cfg>_<kernel>.json of the current kernels
+PROFILE_TAG = "r02f"  # profiles/<tag>_<cfg>_<kernel>.json of the current kernels
 
 
 def profiled_traffic(cfg, kernel):
