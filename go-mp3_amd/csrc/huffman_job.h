@@ -153,35 +153,30 @@ MP3G_HD_INLINE void decode_sym(Reader<kSwap>& r, const uint16_t* T, uint32_t roo
     const uint64_t p64 = r.peek64();
     uint32_t len;
     const uint32_t e = lut_leaf(T, root, (uint32_t)(p64 >> 32), &len);
-    a = (int)((e >> 4) & 15u);
-    b = (int)(e & 15u);
+    const int a0 = (int)((e >> 4) & 15u), b0 = (int)(e & 15u);
     c = kQuad ? (int)((e >> 13) & 1u) : 0;
     d = kQuad ? (int)((e >> 14) & 1u) : 0;
+    // The symbol's length comes from the leaf alone (linbits of a 15, one
+    // sign bit per non-zero value): the next symbol's position does not wait
+    // for the values below, which only feed the stores.
+    const uint32_t na = a0 == 15 ? lb : 0u, nb = b0 == 15 ? lb : 0u;
+    const uint32_t sa = a0 ? 1u : 0u, sb = b0 ? 1u : 0u;
+    r.pos += len + na + sa + nb + sb + (uint32_t)(c + d);
     uint32_t q = (uint32_t)((p64 << len) >> 32);  // the <= 28 bits after the codeword
-    uint32_t o = len;
-    // a: linbits of a 15, then the sign of a non-zero value; the same for b
-    const uint32_t na = a == 15 ? lb : 0u;
-    a += (int)((q >> 1) >> (31u - na));
-    const uint32_t sa = a ? 1u : 0u;
+    a = a0 + (int)((q >> 1) >> (31u - na));
     const bool nega = (q << na) & (sa << 31);
     q <<= na + sa;
-    o += na + sa;
-    const uint32_t nb = b == 15 ? lb : 0u;
-    b += (int)((q >> 1) >> (31u - nb));
-    const uint32_t sb = b ? 1u : 0u;
+    b = b0 + (int)((q >> 1) >> (31u - nb));
     const bool negb = (q << nb) & (sb << 31);
     q <<= nb + sb;
-    o += nb + sb;
     // c, d: quads only (0 / 1, no linbits)
     const bool negc = c && (q >> 31);
     q <<= (uint32_t)c;
     const bool negd = d && (q >> 31);
-    o += (uint32_t)(c + d);
     a = nega ? -a : a;
     b = negb ? -b : b;
     c = negc ? -c : c;
     d = negd ? -d : d;
-    r.pos += o;
   } else {
     const uint32_t e = decode_xy(r, T, root);
     a = (int)((e >> 4) & 15u);
