@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--no-pipelined", action="store_true",
                     help="bitstream leg without the pipelined / io.Reader API runs (profiling: every "
                          "kernel launch then has the timed launches' size)")
+    ap.add_argument("--no-polyphase", action="store_true",
+                    help="skip the standalone polyphase kernel leg (mp3g_plan_synth_execute)")
     return ap.parse_args()
 
 
@@ -231,6 +233,60 @@ def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle, pip
     return out
 
 
+POLY_BYTES_PER_GC = 576 * 4 + 576 * 2  # f32 lines in + s16 PCM out per granule-channel
+
+
+def polyphase_leg(args, rank, dev, stream, d_g, streams, n_gran, local):
+    """The standalone polyphase kernel (mp3g_plan_synth_execute, frame.go:630-688)
+    on the same granules, with synthetic float32 frequency-inverted lines
+    resident in HBM (its cost does not depend on the values): W untimed + K
+    timed launches, HIP events on the launch stream.  roofline on the
+    north star's 3,456 B per granule-channel.  c2 rank 0: max |dPCM| of the
+    timed output against the oracle's subbandSynthesis on the same lines."""
+    import torch
+    import mp3g
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1234 + rank)
+    # magnitudes of real hybrid output (|x| mostly < 0.1, decaying with frequency)
+    d_lines = torch.randn(n_gran, 2, 576, device=dev, generator=gen)
+    d_lines *= 0.05 / (1.0 + torch.arange(576, device=dev, dtype=torch.float32) / 64.0)
+    d_pcm = torch.empty(n_gran * 1152, dtype=torch.int16, device=dev)
+    plan = mp3g.Plan(streams, granules_per_chunk=args.chunk, mode=mp3g.MODE_FAST, device=local)
+    h = stream.cuda_stream
+    for _ in range(args.warmup):
+        plan.synth_execute(d_g, d_lines, d_pcm, stream=h)
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
+    for _ in range(args.steps):
+        plan.synth_execute(d_g, d_lines, d_pcm, stream=h)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    plan.close()
+    ms = ev0.elapsed_time(ev1) / args.steps
+    n_gc = 2 * n_gran  # c2 / c3 are stereo throughout
+    achieved = n_gc * POLY_BYTES_PER_GC / (ms * 1e-3) / 1e9
+    traffic, traffic_src = profiled_traffic(args.config, "granule_synth_kernel")
+    out = {"kernel": "mp3g::v3::granule_synth_kernel", "entry": "mp3g_plan_synth_execute",
+           "kernel_ms": round(ms, 4), "granule_channels_per_s": round(n_gc / (ms * 1e-3), 1),
+           "frames_per_s": round(n_gran / 2 / (ms * 1e-3), 1),
+           "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                        "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": traffic,
+                        "traffic_source": traffic_src, "algorithmic_bytes_per_gc": POLY_BYTES_PER_GC,
+                        "algorithmic_bytes_per_launch": n_gc * POLY_BYTES_PER_GC},
+           "input": "synthetic float32 frequency-inverted lines [n][2][576], device-resident"}
+    if rank == 0 and args.config == "c2" and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle  # checker of the timed output only
+        g_host = d_g.cpu().numpy().view(mp3g.GRANULE_DTYPE)
+        lines = d_lines.cpu().numpy()
+        ref, _ = oracle.synth_streams(g_host, lines, streams)
+        got = d_pcm.cpu().numpy().reshape(-1, 576, 2)
+        out["max_dpcm_lsb"] = int(np.abs(got.astype(np.int32) - ref.astype(np.int32)).max())
+    del d_lines, d_pcm
+    return out
+
+
 PROFILE_TAG = "r02f"  # profiles/<tag>_<cfg>_<kernel>.json of the current kernels
 
 
@@ -331,6 +387,10 @@ def main():
                                   args.steps, args.warmup, check_oracle=rank == 0 and args.config == "c2",
                                   pipelined=not args.no_pipelined)
 
+    polyphase = None
+    if not args.no_polyphase and args.config in ("c2", "c3"):
+        polyphase = polyphase_leg(args, rank, dev, stream, d_g, streams, n_gran, local)
+
     gather_ms = None
     if args.gather and world > 1:
         torch.cuda.synchronize(dev)
@@ -377,6 +437,8 @@ def main():
             out["gather_ms"] = round(gather_ms, 3)
         if bitstream is not None:
             out["bitstream"] = bitstream
+        if polyphase is not None:
+            out["polyphase"] = polyphase
         if world == 1 and not args.no_cpu_baseline and args.config == "c2":
             sys.path.insert(0, os.path.join(REPO, "oracle"))
             import oracle  # CPU baseline leg + parity check of the timed output

@@ -63,4 +63,9 @@ hipError_t launch_fast(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_
                        const int16_t* d_coef, const mp3g_state* d_state_in, mp3g_state* d_state_out,
                        int16_t* d_pcm, unsigned long long* d_stamps, hipStream_t stream);
 
+// Standalone polyphase synthesis (granule_synth.hip, same TU): float32
+// frequency-inverted lines [n][2][576] -> s16 PCM, over a fast-mode plan.
+hipError_t launch_synth(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_granule* d_gran, const float* d_lines,
+                        const mp3g_state* d_state_in, mp3g_state* d_state_out, int16_t* d_pcm, hipStream_t stream);
+
 }  // namespace mp3g

@@ -23,6 +23,7 @@ __constant__ FastTables g_fast;
 
 #include "granule_hdr.h"
 #include "granule_fast.hip"
+#include "granule_synth.hip"
 
 namespace mp3g {
 
@@ -46,6 +47,15 @@ hipError_t launch_fast(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_
   else
     hipLaunchKernelGGL(v3::granule_fast_kernel<false>, grid, block, 0, stream, d_chunks, n_chunks, d_gran, d_coef,
                        d_state_in, d_state_out, d_pcm, nullptr);
+  return hipGetLastError();
+}
+
+hipError_t launch_synth(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_granule* d_gran, const float* d_lines,
+                        const mp3g_state* d_state_in, mp3g_state* d_state_out, int16_t* d_pcm, hipStream_t stream) {
+  if (n_chunks == 0) return hipSuccess;
+  const dim3 grid((n_chunks + v3::kSynthWaves - 1) / v3::kSynthWaves), block(64 * v3::kSynthWaves);
+  hipLaunchKernelGGL(v3::granule_synth_kernel, grid, block, 0, stream, d_chunks, n_chunks, d_gran, d_lines, d_state_in,
+                     d_state_out, d_pcm);
   return hipGetLastError();
 }
 

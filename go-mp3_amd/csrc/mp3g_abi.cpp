@@ -360,6 +360,22 @@ int mp3g_plan_execute(mp3g_plan* p, const mp3g_granule* d_gran, const int16_t* d
   return MP3G_OK;
 }
 
+int mp3g_plan_synth_execute(mp3g_plan* p, const mp3g_granule* d_gran, const float* d_lines,
+                            const mp3g_state* d_state_in, mp3g_state* d_state_out, int16_t* d_pcm, void* hip_stream) {
+  if (!p) return fail(MP3G_ERR_INVALID_ARGUMENT, "null plan");
+  if ((p->mode & 0xffu) != MP3G_MODE_FAST) return fail(MP3G_ERR_INVALID_ARGUMENT, "not a fast-mode plan");
+  if (p->chunks.empty()) return MP3G_OK;
+  if (!d_gran || !d_lines || !d_pcm) return fail(MP3G_ERR_INVALID_ARGUMENT, "null device buffer");
+  DeviceGuard guard(p->device);
+  if (guard.err != hipSuccess) return fail(MP3G_ERR_NO_DEVICE, "hipSetDevice", guard.err);
+  for (const ChunkDesc& c : p->chunks) {
+    if ((c.flags & kChunkStateOut) && !d_state_out) return fail(MP3G_ERR_INVALID_ARGUMENT, "state_out needed");
+  }
+  HIP_TRY(launch_synth(p->d_chunks, (uint32_t)p->chunks.size(), d_gran, d_lines, d_state_in, d_state_out, d_pcm,
+                       static_cast<hipStream_t>(hip_stream)));
+  return MP3G_OK;
+}
+
 int mp3g_huffman_execute(int device, const mp3g_hjob* d_jobs, uint64_t n_granules, const uint8_t* d_md,
                          mp3g_granule* d_gran, int16_t* d_coef, void* hip_stream) {
   if (n_granules == 0) return MP3G_OK;

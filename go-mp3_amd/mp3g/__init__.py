@@ -79,6 +79,7 @@ def lib():
         L.mp3g_plan_destroy.argtypes = [vp]
         L.mp3g_plan_info.argtypes = [vp, C.POINTER(u64), C.POINTER(u64), C.POINTER(u64)]
         L.mp3g_plan_execute.argtypes = [vp, vp, vp, vp, vp, vp, vp]
+        L.mp3g_plan_synth_execute.argtypes = [vp, vp, vp, vp, vp, vp, vp]
         L.mp3g_decode_host.argtypes = [C.c_int, vp, vp, u64, vp, u32, vp, vp, vp, u32]
         L.mp3g_plan_debug_phases.argtypes = [vp, vp, vp, vp, C.POINTER(u64), vp]
         L.mp3g_plan_debug_timeline.argtypes = [vp, vp, vp, vp, C.POINTER(u64), vp]
@@ -492,6 +493,17 @@ class Plan:
         _check(lib().mp3g_plan_execute(self._h, p(d_gran), p(d_coef), p(d_state_in),
                                        p(d_state_out), p(d_pcm),
                                        C.c_void_p(stream) if stream else None))
+
+    def synth_execute(self, d_gran, d_lines, d_pcm, d_state_in=None, d_state_out=None, stream=None):
+        """Standalone polyphase synthesis (mp3g_plan_synth_execute, frame.go:630-688) on
+        float32 frequency-inverted lines [n, 2, 576]; fast-mode plans only."""
+        def p(x):
+            if x is None:
+                return None
+            return C.c_void_p(x.data_ptr() if hasattr(x, "data_ptr") else int(x))
+        _check(lib().mp3g_plan_synth_execute(self._h, p(d_gran), p(d_lines), p(d_state_in),
+                                             p(d_state_out), p(d_pcm),
+                                             C.c_void_p(stream) if stream else None))
 
     PHASES = ("params", "requantize", "stereo+antialias", "imdct", "S rows (transpose)",
               "dct32 (matrixing)", "window+store", "history")

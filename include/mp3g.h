@@ -165,6 +165,18 @@ int mp3g_plan_execute(mp3g_plan* plan, const mp3g_granule* d_granules,
                       const int16_t* d_coeffs, const mp3g_state* d_state_in,
                       mp3g_state* d_state_out, int16_t* d_pcm, void* hip_stream);
 
+/* Standalone polyphase synthesis: go-mp3's subbandSynthesis
+ * (internal/frame/frame.go:630-688, called per channel at frame.go:133) over
+ * the granules of a fast-mode plan, without the stages before it.
+ * d_lines: float32 [n_granules][2][576], the frequency-inverted hybrid output
+ * that subbandSynthesis reads (MainData.Is after frame.go:132; mono granules
+ * leave [g][1][*] unread).  PCM as mp3g_plan_execute (+-1 LSB, fast mode).
+ * State: vvec carried as in mp3g_plan_execute; state_out.store is
+ * state_in.store (or zero), since this stage does not touch it. */
+int mp3g_plan_synth_execute(mp3g_plan* plan, const mp3g_granule* d_granules,
+                            const float* d_lines, const mp3g_state* d_state_in,
+                            mp3g_state* d_state_out, int16_t* d_pcm, void* hip_stream);
+
 /* ---- synchronous host-buffer decode (the cgo drop-in entry) --------------
  * Copies the batch to `device`, decodes it and copies PCM (and state_out)
  * back before returning.  Equivalent to calling Frame.Decode on every frame of

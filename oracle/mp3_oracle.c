@@ -1138,6 +1138,68 @@ int orc_dsp_streams(const mp3g_granule* g, const int16_t* coef, const mp3g_strea
   return 0;
 }
 
+/* Front end + hybrid synthesis only (frame.go:121-133 up to frequencyInversion,
+ * :140-486): writes the float32 lines subbandSynthesis reads, [n][2][576]
+ * (mono: [g][1][*] = 0).  State per stream as orc_dsp_streams (store only;
+ * vVec is not touched by these stages).  Test-input generator for the
+ * standalone polyphase entry point. */
+void orc_hybrid_streams(const mp3g_granule* g, const int16_t* coef, const mp3g_stream* streams,
+                        uint32_t n_streams, const mp3g_state* state_in, float* is_out) {
+  ensure_init();
+  static float store[2][32][18];
+  for (uint32_t s = 0; s < n_streams; s++) {
+    const mp3g_stream* S = &streams[s];
+    if (S->flags & MP3G_STREAM_STATE_IN) memcpy(store, state_in[s].store, sizeof store);
+    else memset(store, 0, sizeof store);
+    for (uint64_t k = S->first_granule; k < S->first_granule + S->n_granules; k++) {
+      gc_fields c[2];
+      float is[2][576];
+      memset(c, 0, sizeof c);
+      const uint32_t h = g[k].header;
+      const int nch = fh_nch(h);
+      for (int ch = 0; ch < 2; ch++) {
+        fields_from_desc(&g[k].ch[ch], &c[ch]);
+        for (int i = 0; i < 576; i++) is[ch][i] = (float)coef[k * 1152 + ch * 576 + i];
+      }
+      const int* sl = SFB_LONG[fh_lsf(h)][fh_sfreq(h)];
+      const int* ss = SFB_SHORT[fh_lsf(h)][fh_sfreq(h)];
+      for (int ch = 0; ch < nch; ch++) {
+        dsp_requantize(&c[ch], sl, ss, is[ch]);
+        dsp_reorder(&c[ch], ss, is[ch]);
+      }
+      dsp_stereo(h, c, sl, ss, is);
+      for (int ch = 0; ch < nch; ch++) {
+        dsp_antialias(&c[ch], is[ch]);
+        dsp_hybrid(&c[ch], is[ch], store[ch]);
+      }
+      if (nch == 1) memset(is[1], 0, sizeof is[1]);
+      memcpy(is_out + k * 1152, is, sizeof is);
+    }
+  }
+}
+
+/* subbandSynthesis alone (frame.go:630-688) over streams of granules whose
+ * frequency-inverted lines are given as float32 [n][2][576]: the semantics of
+ * mp3g_plan_synth_execute.  state: vvec carried per stream (flags as
+ * orc_dsp_streams); state_out.store = state_in.store (or zero), untouched. */
+int orc_synth_streams(const mp3g_granule* g, const float* is, const mp3g_stream* streams,
+                      uint32_t n_streams, const mp3g_state* state_in, mp3g_state* state_out,
+                      int16_t* pcm) {
+  ensure_init();
+  static mp3g_state st;
+  for (uint32_t s = 0; s < n_streams; s++) {
+    const mp3g_stream* S = &streams[s];
+    if (S->flags & MP3G_STREAM_STATE_IN) st = state_in[s];
+    else memset(&st, 0, sizeof st);
+    for (uint64_t k = S->first_granule; k < S->first_granule + S->n_granules; k++) {
+      const int nch = fh_nch(g[k].header);
+      for (int ch = 0; ch < nch; ch++) dsp_synth(nch, ch, is + k * 1152 + ch * 576, st.vvec[ch], pcm + k * 1152);
+    }
+    if (S->flags & MP3G_STREAM_STATE_OUT) state_out[s] = st;
+  }
+  return 0;
+}
+
 typedef struct {
   const mp3g_granule* g;
   const int16_t* coef;

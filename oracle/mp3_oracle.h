@@ -74,6 +74,15 @@ void orc_dsp_granules(const mp3g_granule* g, const int16_t* coef, size_t n, mp3g
 int orc_dsp_streams(const mp3g_granule* g, const int16_t* coef, const mp3g_stream* streams,
                     uint32_t n_streams, const mp3g_state* state_in, mp3g_state* state_out,
                     int16_t* pcm);
+/* Stages before the polyphase (requantize .. frequency inversion) only:
+ * float32 lines [n][2][576] as subbandSynthesis reads them (test inputs). */
+void orc_hybrid_streams(const mp3g_granule* g, const int16_t* coef, const mp3g_stream* streams,
+                        uint32_t n_streams, const mp3g_state* state_in, float* is_out);
+/* subbandSynthesis alone (frame.go:630-688): the semantics of
+ * mp3g_plan_synth_execute (vvec carried; store passed through). */
+int orc_synth_streams(const mp3g_granule* g, const float* is, const mp3g_stream* streams,
+                      uint32_t n_streams, const mp3g_state* state_in, mp3g_state* state_out,
+                      int16_t* pcm);
 /* Multi-threaded wrapper (one stream per task) used only as the CPU baseline. */
 int orc_dsp_streams_mt(const mp3g_granule* g, const int16_t* coef, const mp3g_stream* streams,
                        uint32_t n_streams, int16_t* pcm, int n_threads);

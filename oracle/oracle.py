@@ -61,6 +61,8 @@ def lib():
         L.orc_dsp_granules.argtypes = [vp, vp, sz, vp, vp]
         L.orc_dsp_streams.argtypes = [vp, vp, vp, C.c_uint32, vp, vp, vp]
         L.orc_dsp_streams_mt.argtypes = [vp, vp, vp, C.c_uint32, vp, C.c_int]
+        L.orc_hybrid_streams.argtypes = [vp, vp, vp, C.c_uint32, vp, vp]
+        L.orc_synth_streams.argtypes = [vp, vp, vp, C.c_uint32, vp, vp, vp]
         L.orc_tables.argtypes = [vp] * 6
         L.orc_bits_read.argtypes = [vp, sz, vp, C.c_int, vp, vp]
         L.orc_header_info.argtypes = [C.c_uint32] + [vp] * 6
@@ -116,6 +118,34 @@ def dsp_streams(granules, coeffs, streams, state_in=None):
         state_in = np.zeros(len(streams), STATE_DTYPE)
     L.orc_dsp_streams(_ptr(granules), _ptr(coeffs), _ptr(streams), len(streams), _ptr(state_in),
                       _ptr(state_out), _ptr(pcm))
+    return pcm, state_out
+
+
+def hybrid_streams(granules, coeffs, streams, state_in=None):
+    """Stages before the polyphase (frame.go:140-486): float32 lines [n, 2, 576]."""
+    L = lib()
+    granules = np.ascontiguousarray(granules, dtype=GRANULE_DTYPE)
+    coeffs = np.ascontiguousarray(coeffs, dtype=np.int16)
+    streams = np.ascontiguousarray(streams, dtype=STREAM_DTYPE)
+    out = np.zeros((len(granules), 2, 576), np.float32)
+    if state_in is None:
+        state_in = np.zeros(len(streams), STATE_DTYPE)
+    L.orc_hybrid_streams(_ptr(granules), _ptr(coeffs), _ptr(streams), len(streams), _ptr(state_in), _ptr(out))
+    return out
+
+
+def synth_streams(granules, lines, streams, state_in=None):
+    """subbandSynthesis alone (frame.go:630-688) on float32 lines [n, 2, 576]."""
+    L = lib()
+    granules = np.ascontiguousarray(granules, dtype=GRANULE_DTYPE)
+    lines = np.ascontiguousarray(lines, dtype=np.float32)
+    streams = np.ascontiguousarray(streams, dtype=STREAM_DTYPE)
+    pcm = np.zeros((len(granules), 576, 2), np.int16)
+    state_out = np.zeros(len(streams), STATE_DTYPE)
+    if state_in is None:
+        state_in = np.zeros(len(streams), STATE_DTYPE)
+    L.orc_synth_streams(_ptr(granules), _ptr(lines), _ptr(streams), len(streams), _ptr(state_in),
+                        _ptr(state_out), _ptr(pcm))
     return pcm, state_out
 
 

@@ -125,9 +125,11 @@ def test_exact_kernel_has_no_fma():
     asm = open(os.path.join(csrc, "build", "kernels.s")).read() + \
         open(os.path.join(csrc, "build", "kernels_fast.s")).read()
     kernels = re.findall(r"^(_ZN4mp3g2v\d\w+kernel\w*):(.*?)\.end_amdhsa_kernel", asm, re.S | re.M)
-    exact = [(n, b) for n, b in kernels if "granule_fast" not in n]
-    fast = [(n, b) for n, b in kernels if "granule_fast" in n]
-    assert len(exact) >= 2 and len(fast) >= 1, [k[0] for k in kernels]
+    # fast-mode kernels: the fused v3 kernel and the standalone polyphase kernel
+    is_fast = lambda n: "granule_fast" in n or "granule_synth" in n  # noqa: E731
+    exact = [(n, b) for n, b in kernels if not is_fast(n)]
+    fast = [(n, b) for n, b in kernels if is_fast(n)]
+    assert len(exact) >= 2 and len(fast) >= 2, [k[0] for k in kernels]
     # the fast kernel (+-1 LSB mode) is the one allowed -- and expected -- to contract
     assert all(re.search(r"\bv_(pk_)?fmac?_f32", b) for _, b in fast), "fast kernel lost its FMAs"
     for name, body in exact:

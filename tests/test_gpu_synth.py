@@ -1,0 +1,119 @@
+"""GPU parity of the standalone polyphase kernel (mp3g_plan_synth_execute,
+granule_synth.hip) vs the oracle's subbandSynthesis (frame.go:630-688).
+
+Inputs are the float32 frequency-inverted lines the reference hands to
+subbandSynthesis, produced by the oracle's own front end + hybrid synthesis
+(orc_hybrid_streams) from the sample files and seeded synthetic granules.
+Bar: +-1 LSB (the fast mode's reassociated matrixing and window, north-star
+tolerance), differing samples < 1 %, vVec state within float tolerance, and
+chunking bit-identical to a one-chunk (serial) run.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from mp3g import synth
+from test_gpu_fast import assert_close
+from test_gpu_parity import SYNTH_CASES
+
+pytestmark = pytest.mark.gpu
+
+
+def run_synth(mp3g, g, lines, streams, chunk=0, state_in=None):
+    import torch
+    n = len(g)
+    dev = torch.device("cuda")
+    d_g = torch.from_numpy(np.ascontiguousarray(g).view(np.uint8).reshape(-1).copy()).to(dev)
+    d_l = torch.from_numpy(np.ascontiguousarray(lines, dtype=np.float32).reshape(-1).copy()).to(dev)
+    d_pcm = torch.zeros(max(n, 1) * 2304, dtype=torch.uint8, device=dev)
+    d_si = (torch.from_numpy(np.ascontiguousarray(state_in).view(np.uint8).reshape(-1).copy()).to(dev)
+            if state_in is not None else None)
+    d_so = torch.zeros(len(streams) * mp3g.STATE_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    plan = mp3g.Plan(streams, granules_per_chunk=chunk, mode=mp3g.MODE_FAST)
+    plan.synth_execute(d_g, d_l, d_pcm, d_si, d_so, stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    pcm = d_pcm.cpu().numpy().view(np.int16)[: n * 1152].reshape(n, 576, 2)
+    so = d_so.cpu().numpy().view(mp3g.STATE_DTYPE)
+    plan.close()
+    return pcm, so
+
+
+@pytest.mark.parametrize("name", ["classic_lame.mp3", "mpeg2.mp3"])
+def test_synth_sample_files(gpu, captured, name):
+    g, c, want = captured[name]
+    s = gpu.streams_for([len(g)], gpu.STATE_OUT)
+    lines = oracle.hybrid_streams(g, c, s)
+    ref, so_ref = oracle.synth_streams(g, lines, s)
+    assert np.array_equal(ref, want)  # the split oracle is the whole-frame oracle
+    serial, so_serial = run_synth(gpu, g, lines, s, chunk=len(g))
+    assert_close(serial, want, name)
+    np.testing.assert_allclose(so_serial["vvec"], so_ref["vvec"], rtol=0, atol=2e-5)
+    for chunk in (1, 2, 7, 64, 0):
+        pcm, so = run_synth(gpu, g, lines, s, chunk=chunk)
+        assert np.array_equal(pcm, serial), f"{name} chunk={chunk} differs from the serial run"
+        assert so.tobytes() == so_serial.tobytes(), f"{name} chunk={chunk}: exported state differs"
+
+
+@pytest.mark.parametrize("case", sorted(SYNTH_CASES))
+def test_synth_synthetic_batches(gpu, case):
+    g, c, s = synth.synth_batch(6, 60, seed=300 + len(case), **SYNTH_CASES[case])
+    lines = oracle.hybrid_streams(g, c, s)
+    want, _ = oracle.synth_streams(g, lines, s)
+    pcm, _ = run_synth(gpu, g, lines, s)
+    assert_close(pcm, want, case)
+    for chunk in (1, 3):
+        assert np.array_equal(run_synth(gpu, g, lines, s, chunk=chunk)[0], pcm), f"{case} chunk={chunk}"
+
+
+def test_synth_mono_stereo_switch_and_state(gpu):
+    parts = [synth.synth_stream(21, 6), synth.synth_stream(22, 9, mode=synth.MODE_MONO),
+             synth.synth_stream(23, 4), synth.synth_stream(24, 3, mode=synth.MODE_MONO),
+             synth.synth_stream(25, 5)]
+    g = np.concatenate([p[0] for p in parts])
+    c = np.concatenate([p[1] for p in parts])
+    n = len(g)
+    # two streams over the same granules: the second starts from a state
+    # (that of the oracle after 5 granules of the first)
+    _, st5 = oracle.dsp_streams(g[:5], c[:5], gpu.streams_for([5], gpu.STATE_OUT))
+    g2 = np.concatenate([g, g])
+    c2 = np.concatenate([c, c])
+    s = gpu.streams_for([n, n], gpu.STATE_OUT)
+    s["flags"][1] |= gpu.STATE_IN
+    st_in = np.zeros(2, gpu.STATE_DTYPE)
+    st_in[1] = st5[0]
+    lines = oracle.hybrid_streams(g2, c2, s, state_in=st_in)
+    want, so_ref = oracle.synth_streams(g2, lines, s, state_in=st_in)
+    serial, so_serial = run_synth(gpu, g2, lines, s, chunk=n, state_in=st_in)
+    assert_close(serial, want, "switch serial")
+    np.testing.assert_allclose(so_serial["vvec"], so_ref["vvec"], rtol=0, atol=2e-5)
+    assert so_serial["store"].tobytes() == so_ref["store"].tobytes()  # passed through
+    for chunk in (1, 2, 5, 0):
+        pcm, so = run_synth(gpu, g2, lines, s, chunk=chunk, state_in=st_in)
+        assert np.array_equal(pcm, serial), f"chunk={chunk}"
+        assert so.tobytes() == so_serial.tobytes(), f"chunk={chunk}: state"
+
+
+def test_synth_silence_and_clipping(gpu):
+    g, c, s = synth.synth_batch(1, 8, seed=3)
+    zeros = np.zeros((len(g), 2, 576), np.float32)
+    pcm, _ = run_synth(gpu, g, zeros, s)
+    assert not pcm.any()
+    loud = np.full((len(g), 2, 576), 1e4, np.float32)
+    loud[:, :, 1::2] *= -1
+    want, _ = oracle.synth_streams(g, loud, s)
+    got, _ = run_synth(gpu, g, loud, s)
+    assert_close(got, want, "clipping")
+    assert np.abs(got.astype(np.int32)).max() == 32767
+
+
+def test_synth_empty_plan_and_errors(gpu):
+    import torch
+    s = gpu.streams_for([])
+    plan = gpu.Plan(s, mode=gpu.MODE_FAST)
+    plan.synth_execute(None, None, None)  # nothing to do: no pointers needed
+    plan.close()
+    exact = gpu.Plan(gpu.streams_for([4]), mode=gpu.MODE_EXACT)
+    x = torch.zeros(16, dtype=torch.uint8, device="cuda")
+    with pytest.raises(Exception):
+        exact.synth_execute(x, x, x)  # standalone synthesis runs on fast-mode plans only
+    exact.close()
