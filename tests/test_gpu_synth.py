@@ -19,6 +19,14 @@ from test_gpu_parity import SYNTH_CASES
 pytestmark = pytest.mark.gpu
 
 
+def assert_vvec_close(got, want):
+    """The 15 newest V blocks, which are all any later window reads
+    (frame.go:649-660); the kernels export the oldest (16th) block as zeros,
+    as the fused kernels do."""
+    np.testing.assert_allclose(got["vvec"][..., :960], want["vvec"][..., :960], rtol=0, atol=2e-5)
+    assert not got["vvec"][..., 960:].any()
+
+
 def run_synth(mp3g, g, lines, streams, chunk=0, state_in=None):
     import torch
     n = len(g)
@@ -47,7 +55,7 @@ def test_synth_sample_files(gpu, captured, name):
     assert np.array_equal(ref, want)  # the split oracle is the whole-frame oracle
     serial, so_serial = run_synth(gpu, g, lines, s, chunk=len(g))
     assert_close(serial, want, name)
-    np.testing.assert_allclose(so_serial["vvec"], so_ref["vvec"], rtol=0, atol=2e-5)
+    assert_vvec_close(so_serial, so_ref)
     for chunk in (1, 2, 7, 64, 0):
         pcm, so = run_synth(gpu, g, lines, s, chunk=chunk)
         assert np.array_equal(pcm, serial), f"{name} chunk={chunk} differs from the serial run"
@@ -85,7 +93,7 @@ def test_synth_mono_stereo_switch_and_state(gpu):
     want, so_ref = oracle.synth_streams(g2, lines, s, state_in=st_in)
     serial, so_serial = run_synth(gpu, g2, lines, s, chunk=n, state_in=st_in)
     assert_close(serial, want, "switch serial")
-    np.testing.assert_allclose(so_serial["vvec"], so_ref["vvec"], rtol=0, atol=2e-5)
+    assert_vvec_close(so_serial, so_ref)
     assert so_serial["store"].tobytes() == so_ref["store"].tobytes()  # passed through
     for chunk in (1, 2, 5, 0):
         pcm, so = run_synth(gpu, g2, lines, s, chunk=chunk, state_in=st_in)
@@ -98,8 +106,10 @@ def test_synth_silence_and_clipping(gpu):
     zeros = np.zeros((len(g), 2, 576), np.float32)
     pcm, _ = run_synth(gpu, g, zeros, s)
     assert not pcm.any()
-    loud = np.full((len(g), 2, 576), 1e4, np.float32)
-    loud[:, :, 1::2] *= -1
+    # a loud low-frequency tone: subband 0 of both channels at 4.0 (PCM far
+    # past full scale without the cancellation of huge alternating values)
+    loud = np.zeros((len(g), 2, 576), np.float32)
+    loud[:, :, :18] = 4.0
     want, _ = oracle.synth_streams(g, loud, s)
     got, _ = run_synth(gpu, g, loud, s)
     assert_close(got, want, "clipping")
