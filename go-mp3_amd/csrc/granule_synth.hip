@@ -33,6 +33,17 @@ namespace v3 {
 #define MP3G_SYNTH_WG_WAVES 8
 #endif
 constexpr int kSynthWaves = MP3G_SYNTH_WG_WAVES;
+// granules of lines in flight per wave (register buffers of 18 VGPRs)
+#ifndef MP3G_SYNTH_DEPTH
+#define MP3G_SYNTH_DEPTH 1  // 2 measured the same at c3 and 2 % slower at c2
+#endif
+// cache-policy bits of the line loads / PCM stores (experiments)
+#ifndef MP3G_SYNTH_LOAD_AUX
+#define MP3G_SYNTH_LOAD_AUX 0
+#endif
+#ifndef MP3G_SYNTH_STORE_AUX
+#define MP3G_SYNTH_STORE_AUX 0
+#endif
 
 struct __align__(16) SynthWaveSmem {
   float ring[2][32][kSlots];
@@ -83,26 +94,26 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
     }
   }
 
-  // the granule's lines as 8-B pairs: pair p = lane + 64 r of [nch][576]
-  auto load = [&](uint32_t g, uint32_t nch, f2 v[9]) {
+  // the granule's lines as 8-B pairs: pair p = lane + 64 r of [nch][576].
+  // Issued unconditionally (straight-line vmcnt accounting): past the chunk
+  // the resource has no records, so the loads return 0 and touch no memory.
+  auto load = [&](uint32_t g, f2 v[9]) {
+    const bool in = g < end;
+    const uint32_t gg = in ? g : w;
+    const uint32_t nch = in ? hdr_nch(__builtin_amdgcn_readfirstlane(gran[gg].header)) : 0u;
     const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(lines + (size_t)g * MP3G_COEF_PER_GRANULE), (short)0, (int)(nch * 2304u), 0x00020000);
+        const_cast<float*>(lines + (size_t)gg * MP3G_COEF_PER_GRANULE), (short)0, (int)(nch * 2304u), 0x00020000);
 #pragma unroll
     for (int r = 0; r < 9; r++) {
-      const auto u = __builtin_amdgcn_raw_buffer_load_b64(rc, 8 * lane + 512 * r, 0, 0);
+      const auto u = __builtin_amdgcn_raw_buffer_load_b64(rc, 8 * lane + 512 * r, 0, MP3G_SYNTH_LOAD_AUX);
       v[r] = (f2){__uint_as_float(u[0]), __uint_as_float(u[1])};
     }
   };
-  f2 cur[9];
-  uint32_t h = 0;
-  if (w < end) {
-    h = __builtin_amdgcn_readfirstlane(gran[w].header);
-    load(w, hdr_nch(h), cur);
-  }
-  wave_sync();
   const int hi = lane >> 5;
 
-  for (uint32_t g = w; g < end; g++) {
+  // one granule; its lines in `buf`, which is refilled with granule g + depth
+  auto granule = [&](uint32_t g, f2 buf[9]) {
+    const uint32_t h = __builtin_amdgcn_readfirstlane(gran[g].header);
     const int nch = hdr_nch(h);
     const bool out = g >= out_first;
     // ---- stage: line 18 sb + ss of channel c -> ring[c][sb][16 + ss] ----
@@ -112,15 +123,10 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
       const int c = e >= 576;
       const int l = e - 576 * c;
       const int sb = (l * 3641) >> 16;  // l / 18 for l < 576
-      if (c < nch) *reinterpret_cast<f2*>(&s.ring[c][sb][kHist + l - 18 * sb]) = cur[r];
+      if (c < nch) *reinterpret_cast<f2*>(&s.ring[c][sb][kHist + l - 18 * sb]) = buf[r];
     }
-    // next granule in flight during the matrixing and window
-    const bool more = g + 1 < end;
-    uint32_t hn = h;
-    if (more) {
-      hn = __builtin_amdgcn_readfirstlane(gran[g + 1].header);
-      load(g + 1, hdr_nch(hn), cur);
-    }
+    // a later granule in flight during the matrixing and window
+    load(g + MP3G_SYNTH_DEPTH, buf);
     wave_sync();
     // ---- matrixing (frame.go:642-648): lane (ch, slot) turns its S row into X ----
     {
@@ -137,7 +143,9 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
       }
     }
     wave_sync();
-    // ---- 16-tap window -> s16 PCM (frame.go:649-678) ----
+    // ---- 16-tap window -> s16 PCM (frame.go:649-678); the stores are issued
+    //      for replayed granules too, through a resource with no records ----
+    uint32_t pk[9] = {};  // (dropped for replayed granules)
     if (out) {
       float dw[16];
       {
@@ -169,7 +177,6 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
           }
         }
       }
-      uint32_t pk[9];
       auto pack = [&](auto mono) {
 #pragma unroll
         for (int p = 0; p < 9; p++) {
@@ -181,9 +188,13 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
       };
       if (nch == 2) pack(std::false_type{});
       else pack(std::true_type{});
-      uint32_t* P = reinterpret_cast<uint32_t*>(pcm + (size_t)g * 1152);
+    }
+    {
+      const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
+          pcm + (size_t)g * 1152, (short)0, out ? MP3G_PCM_BYTES_PER_GRANULE : 0, 0x00020000);
 #pragma unroll
-      for (int p = 0; p < 9; p++) P[32 * (2 * p + hi) + k] = pk[p];
+      for (int p = 0; p < 9; p++)
+        __builtin_amdgcn_raw_buffer_store_b32(pk[p], rp, 4 * (32 * (2 * p + hi) + k), 0, MP3G_SYNTH_STORE_AUX);
     }
     wave_sync();
     // ---- history shift of the channels this granule touched ----
@@ -193,8 +204,24 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
       for (int q = 0; q < 8; q++) col[q] = col[9 + q];
     }
     wave_sync();
-    h = hn;
+  };
+
+#if MP3G_SYNTH_DEPTH == 1
+  f2 A[9];
+  load(w, A);
+  wave_sync();
+  for (uint32_t g = w; g < end; g++) granule(g, A);
+#else
+  // two granules in flight: ping-pong buffers, the loop unrolled by two
+  f2 A[9], B[9];
+  load(w, A);
+  load(w + 1, B);
+  wave_sync();
+  for (uint32_t g = w; g < end; g += 2) {
+    granule(g, A);
+    if (g + 1 < end) granule(g + 1, B);
   }
+#endif
 
   if (cd.flags & kChunkStateOut) {
     // vVec out; the IMDCT overlap `store` is not this stage's: passed through
