@@ -37,6 +37,9 @@ constexpr int kSynthWaves = MP3G_SYNTH_WG_WAVES;
 #ifndef MP3G_SYNTH_DEPTH
 #define MP3G_SYNTH_DEPTH 1  // 2 measured the same at c3 and 2 % slower at c2
 #endif
+#ifndef MP3G_SYNTH_PRIO
+#define MP3G_SYNTH_PRIO 1  // c2 -3.5 %, c3 +-0 (tools/gpu_synthab.sh)
+#endif
 // cache-policy bits of the line loads / PCM stores (experiments)
 #ifndef MP3G_SYNTH_LOAD_AUX
 #define MP3G_SYNTH_LOAD_AUX 0
@@ -49,7 +52,10 @@ struct __align__(16) SynthWaveSmem {
   float ring[2][32][kSlots];
 };
 
-__global__ void __launch_bounds__(kLanes * kSynthWaves, 4)
+#ifndef MP3G_SYNTH_WAVES_PER_SIMD
+#define MP3G_SYNTH_WAVES_PER_SIMD 4
+#endif
+__global__ void __launch_bounds__(kLanes * kSynthWaves, MP3G_SYNTH_WAVES_PER_SIMD)
 granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, const mp3g_granule* __restrict__ gran,
                      const float* __restrict__ lines, const mp3g_state* __restrict__ state_in,
                      mp3g_state* __restrict__ state_out, int16_t* __restrict__ pcm) {
@@ -210,7 +216,20 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
   f2 A[9];
   load(w, A);
   wave_sync();
-  for (uint32_t g = w; g < end; g++) granule(g, A);
+#if MP3G_SYNTH_PRIO
+  const uint32_t span = end - w, span2 = 2 * span, span3 = 3 * span;
+#endif
+  for (uint32_t g = w; g < end; g++) {
+#if MP3G_SYNTH_PRIO
+    // progress-balanced issue priority, as in the fused kernel
+    const uint32_t left4 = 4u * (end - g);
+    if (left4 > span3) __builtin_amdgcn_s_setprio(3);
+    else if (left4 > span2) __builtin_amdgcn_s_setprio(2);
+    else if (left4 > span) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+#endif
+    granule(g, A);
+  }
 #else
   // two granules in flight: ping-pong buffers, the loop unrolled by two
   f2 A[9], B[9];
