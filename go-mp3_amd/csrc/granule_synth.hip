@@ -37,6 +37,9 @@ constexpr int kSynthWaves = MP3G_SYNTH_WG_WAVES;
 #ifndef MP3G_SYNTH_DEPTH
 #define MP3G_SYNTH_DEPTH 1  // 2 measured the same at c3 and 2 % slower at c2
 #endif
+#ifndef MP3G_SYNTH_DW_REGS
+#define MP3G_SYNTH_DW_REGS 1
+#endif
 #ifndef MP3G_SYNTH_PRIO
 #define MP3G_SYNTH_PRIO 1  // c2 -3.5 %, c3 +-0 (tools/gpu_synthab.sh)
 #endif
@@ -116,6 +119,22 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
     }
   };
   const int hi = lane >> 5;
+  // the lane's 16 window taps, in registers for the whole chunk (read per
+  // granule they were four 4-way bank-conflicted ds_read_b128)
+  float dw[16];
+#if MP3G_SYNTH_DW_REGS
+  {
+    const float4* d4 = reinterpret_cast<const float4*>(&dwin_s[k][0]);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const float4 v = d4[q];
+      dw[4 * q] = v.x;
+      dw[4 * q + 1] = v.y;
+      dw[4 * q + 2] = v.z;
+      dw[4 * q + 3] = v.w;
+    }
+  }
+#endif
 
   // one granule; its lines in `buf`, which is refilled with granule g + depth
   auto granule = [&](uint32_t g, f2 buf[9]) {
@@ -129,7 +148,10 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
       const int c = e >= 576;
       const int l = e - 576 * c;
       const int sb = (l * 3641) >> 16;  // l / 18 for l < 576
-      if (c < nch) *reinterpret_cast<f2*>(&s.ring[c][sb][kHist + l - 18 * sb]) = buf[r];
+      // indexed as 8-B pairs (ds_write_b64, 4 x 16 lanes): as separate dwords
+      // the 32 lanes of a write group land on 16 even banks
+      f2* colp = reinterpret_cast<f2*>(&s.ring[c][0][0]);
+      if (c < nch) colp[17 * sb + kHist / 2 + ((l - 18 * sb) >> 1)] = buf[r];
     }
     // a later granule in flight during the matrixing and window
     load(g + MP3G_SYNTH_DEPTH, buf);
@@ -153,7 +175,7 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
     //      for replayed granules too, through a resource with no records ----
     uint32_t pk[9] = {};  // (dropped for replayed granules)
     if (out) {
-      float dw[16];
+#if !MP3G_SYNTH_DW_REGS
       {
         const float4* d4 = reinterpret_cast<const float4*>(&dwin_s[k][0]);
 #pragma unroll
@@ -165,6 +187,7 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
           dw[4 * q + 3] = v.w;
         }
       }
+#endif
       const f2* RA = reinterpret_cast<const f2*>(&s.ring[ch][pa][0]);
       const float* RB = &s.ring[ch][pb][0];
       f2 acc2[9];
