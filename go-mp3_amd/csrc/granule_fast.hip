@@ -86,6 +86,10 @@ constexpr int kHist = 16;
 #define MP3G_FAST_WAVES_PER_SIMD 4
 #endif
 constexpr int kSlots = kHist + 18;
+#ifndef MP3G_FAST_DWIN_STRIDE
+#define MP3G_FAST_DWIN_STRIDE 20
+#endif
+constexpr int kDwinStride = MP3G_FAST_DWIN_STRIDE;
 
 // read-only tables, one copy per workgroup
 struct __align__(16) SharedSmem {
@@ -95,7 +99,10 @@ struct __align__(16) SharedSmem {
   // sign of its line in an odd subband (frame.go:480-486)
   float4 winp[4][2][9];
   float isr[8][2];
-  float dwin[32][16];  // FastTables::dwin rows, pre-scaled by 32767
+  // FastTables::dwin rows, pre-scaled by 32767, padded to 20 floats: the
+  // lanes of a ds_read_b128 group (4 x 16) then hit 16 distinct bank quads
+  // (16-float rows put every fourth row on one quad: 4-way conflicts)
+  float dwin[32][kDwinStride];
   // FastTables::lband: read per lane every granule, so it lives in LDS -- a
   // vector global load there would wait (vmcnt is in order) for the previous
   // granule's PCM stores
@@ -281,7 +288,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     }
     // is_pos 0..6 -> isRatios (frame.go:304-306); 7 -> (1, 1): no change
     for (int e = t; e < 16; e += kLanes * kWaves) (&sh.isr[0][0])[e] = e < 14 ? (&g_fast.is_ratio[0][0])[e] : 1.0f;
-    for (int e = t; e < 32 * 16; e += kLanes * kWaves) (&sh.dwin[0][0])[e] = (&g_fast.dwin[0][0])[e] * 32767.0f;
+    for (int e = t; e < 32 * 16; e += kLanes * kWaves) sh.dwin[e >> 4][e & 15] = (&g_fast.dwin[0][0])[e] * 32767.0f;
     for (int e = t; e < kCombos * 32; e += kLanes * kWaves) (&sh.lband[0][0])[e] = (&g_fast.lband[0][0])[e];
   }
   __syncthreads();  // the only workgroup barrier: the waves are independent from here on
