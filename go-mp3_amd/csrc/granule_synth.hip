@@ -48,7 +48,7 @@ constexpr int kSynthWaves = MP3G_SYNTH_WG_WAVES;
 #define MP3G_SYNTH_LOAD_AUX 0
 #endif
 #ifndef MP3G_SYNTH_STORE_AUX
-#define MP3G_SYNTH_STORE_AUX 0
+#define MP3G_SYNTH_STORE_AUX 2  // non-temporal PCM stores: c3 -1.3 %, c2 -2 % (the lines: nt loads +5 %)
 #endif
 
 struct __align__(16) SynthWaveSmem {
