@@ -86,6 +86,9 @@ constexpr int kHist = 16;
 #define MP3G_FAST_WAVES_PER_SIMD 4
 #endif
 constexpr int kSlots = kHist + 18;
+#ifndef MP3G_FAST_STRAIGHT
+#define MP3G_FAST_STRAIGHT 1
+#endif
 #ifndef MP3G_FAST_NT_STORE
 #define MP3G_FAST_NT_STORE 1  // non-temporal PCM stores: c2 -1.9 %, c3 -0.8 % (tools/gpu_ab.sh)
 #endif
@@ -129,10 +132,11 @@ struct __align__(16) WaveSmem {
 // Raw coefficients of lane (ch, sb) of granule g: its 18 lines, 36 B at
 // coef[g][ch][18 sb], as 9 dwords (two int16 each) by three 12-B buffer loads
 // through a per-granule resource (SGPR base, 32-bit lane offset).
-__device__ __forceinline__ void load_lines(const int16_t* coef, uint32_t g, int lane, uint32_t cw[9]) {
+// (nbytes = 0: a resource without records -- the loads return 0 and touch no memory)
+__device__ __forceinline__ void load_lines(const int16_t* coef, uint32_t g, int lane, uint32_t cw[9],
+                                           int nbytes = (int)(MP3G_COEF_PER_GRANULE * sizeof(int16_t))) {
   const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<int16_t*>(coef + (size_t)g * MP3G_COEF_PER_GRANULE), (short)0,
-      (int)(MP3G_COEF_PER_GRANULE * sizeof(int16_t)), 0x00020000);
+      const_cast<int16_t*>(coef + (size_t)g * MP3G_COEF_PER_GRANULE), (short)0, nbytes, 0x00020000);
   const int off = (lane >> 5) * 1152 + (lane & 31) * 36;
 #pragma unroll
   for (int i = 0; i < 3; i++) {
@@ -353,7 +357,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
   wave_sync();
 
   // PCM of a granule: one dword (L, R) per lane and slot pair
-  uint32_t pk[9];
+  uint32_t pk[9] = {};
   const int hi = lane >> 5;
 
   if constexpr (kStamp) {
@@ -685,6 +689,19 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     // prefetch
     const bool more = g + 1 < end;
     uint4 pd = {0, 0, 0, 0};
+#if MP3G_FAST_STRAIGHT
+    // issued unconditionally (straight-line vmcnt accounting, as the PCM
+    // stores below): past the chunk the resources have no records
+    {
+      load_lines(coef, g + 1, lane, cw, more ? (int)(MP3G_COEF_PER_GRANULE * sizeof(int16_t)) : 0);
+      if (lane < 10) {
+        const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<mp3g_granule*>(gran + g + 1), (short)0, more ? (int)sizeof(mp3g_granule) : 0, 0x00020000);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rd, lane * 16, 0, 0);
+        pd = make_uint4(v[0], v[1], v[2], v[3]);
+      }
+    }
+#else
     if (more) {
       load_lines(coef, g + 1, lane, cw);
       if (lane < 10) {
@@ -694,6 +711,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
         pd = make_uint4(v[0], v[1], v[2], v[3]);
       }
     }
+#endif
 
     // ---- matrixing (frame.go:642-648): S rows into the ring (lane (ch, sb)
     //      writes its 18 slots), then one lane per (ch, slot) turns its row into
@@ -798,6 +816,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       // stored right away: a store's data registers are free again once it
       // has issued (no s_waitcnt before their reuse on gfx950), and the loads
       // this wave waits for next were issued before these stores
+#if !MP3G_FAST_STRAIGHT
       uint32_t* P = reinterpret_cast<uint32_t*>(pcm + (size_t)g * 1152);
 #pragma unroll
       for (int p = 0; p < 9; p++) {
@@ -807,7 +826,18 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
         P[32 * (2 * p + hi) + k] = pk[p];
 #endif
       }
+#endif
     }
+#if MP3G_FAST_STRAIGHT
+    {
+      // issued for replayed granules too, through a resource with no records
+      const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
+          pcm + (size_t)g * 1152, (short)0, out ? MP3G_PCM_BYTES_PER_GRANULE : 0, 0x00020000);
+#pragma unroll
+      for (int p = 0; p < 9; p++)
+        __builtin_amdgcn_raw_buffer_store_b32(pk[p], rp, 4 * (32 * (2 * p + hi) + k), 0, MP3G_FAST_NT_STORE ? 2 : 0);
+    }
+#endif
 #ifndef MP3G_EXP_NOSYNC_SHIFT
     wave_sync();  // ring reads done
 #endif
