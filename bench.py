@@ -287,7 +287,7 @@ def polyphase_leg(args, rank, dev, stream, d_g, streams, n_gran, local):
     return out
 
 
-PROFILE_TAG = "r02h"  # profiles/<tag>_<cfg>_<kernel>.json of the current kernels
+PROFILE_TAG = "r02i"  # profiles/<tag>_<cfg>_<kernel>.json of the current kernels
 
 
 def profiled_traffic(cfg, kernel):
