@@ -71,6 +71,11 @@ struct FastTables {
   float win[4][36];
   float dct[32][16];
   float dwin[32][16];
+  // reference-order fallback (hot granules, granule_fast.hip): the full rows
+  // of the 32 distinct V values, X[m] = sum_j nrow[m][j] S[j] in the
+  // reference's summation order -- nrow[m] = synthNWin[m-16] (m >= 16),
+  // -synthNWin[48-m] (m < 16), negated rows giving bit-negated sums
+  float nrow[32][32];
   float aa_cs[8], aa_ca[8];
   float is_ratio[8][2];           // [is_pos][ch] (rows 0..6 used)
   // per (combo, output line L): the line's long band (bits 0..4), short band

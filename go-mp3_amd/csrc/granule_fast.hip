@@ -6,26 +6,28 @@
 // of the reference instead of bit-identical (north star tolerance; measured
 // by tests/test_gpu_parity.py::test_fast_mode_*).
 //
-// Work decomposition: ONE WAVE PER CHUNK.  A 64-lane workgroup walks its chunk
-// granule by granule with no s_barrier-level cross-wave traffic:
-//   front end   lane = (ch, sb): the 18 lines of its subband -- requantize
-//               (gather through the reorder table), MS/IS with the partner
-//               channel via a lane^32 shuffle, antialias butterflies with the
-//               neighbouring subbands via lane+-1 shuffles;
-//   IMDCT       lane = (ch, sb): 36-point (or 3 x 12-point) IMDCT in registers,
-//               the overlap `store` lives in the lane's VGPRs for the whole
-//               chunk, frequency inversion;
-//   matrixing   V = synthNWin * S has 32 distinct values X (DSP identity,
-//               dsp_tables.h FastTables); the lane pair (sb, 31-sb) folds
-//               S into even/odd halves (lane^31 shuffle), then lane = (ch, m)
-//               computes X_m for all 18 time slots: 16 FMAs per value against
-//               its coefficient row held in VGPRs;
-//   window      lane = (ch, i): 16-tap window over the X ring with the V->X
-//               signs folded into the taps (VGPRs), 18 outputs per lane, s16
-//               packed (L,R) with one lane^32 exchange per slot pair.
-// LDS per wave ~14 KB (raw/eo union, X ring 2 x 34 x 32, descriptor, IMDCT
-// windows) -> 11 resident waves per CU.
-// (compiled as part of kernels.hip, after granule_common.hip)
+// Work decomposition: ONE WAVE PER CHUNK, eight independent waves (chunks)
+// per 512-thread workgroup sharing the read-only tables, 16 waves per CU
+// (<= 128 VGPRs, 9.1 KB of LDS per wave + 4 KB shared).  A wave walks its
+// chunk granule by granule with wave-level LDS ordering only:
+//   front end   lane = (ch, sb): the 18 lines of its subband from registers
+//               (prefetched one granule ahead) -- requantize as
+//               x 2^(log2|x|/3 + n4/4), short blocks through an LDS gather
+//               (the reorder); MS pairs through v_permlane32_swap, intensity
+//               stereo per lane; antialias butterflies via DPP wave shifts;
+//   IMDCT       lane = (ch, sb): long blocks as a packed DCT-IV-18
+//               (dct4_18.h), the overlap `store` in the lane's VGPRs for the
+//               whole chunk, frequency inversion folded into window signs;
+//   matrixing   V = synthNWin * S has 32 distinct values X: lane = (ch, slot)
+//               runs an in-lane fast DCT-II-32 on float pairs (dct32.h) over
+//               its column of the X ring, in place;
+//   window      lane = (ch, i): 16 taps (V->X signs and x32767 folded in)
+//               over operand pairs of the column-major ring, s16 (L, R) pairs
+//               through one v_permlane32_swap per slot pair, stored at once.
+// Hot granules (hybrid output above kHotS) run the same stages in the
+// reference's operation order (the *_exact functions) after a rewind of the
+// wave to the granule's replay start: PCM within +-1 LSB on every valid input.
+// (compiled in its own TU, kernels_fast.hip)
 #pragma clang fp contract(fast)
 #include <type_traits>
 
@@ -86,12 +88,6 @@ constexpr int kHist = 16;
 #define MP3G_FAST_WAVES_PER_SIMD 4
 #endif
 constexpr int kSlots = kHist + 18;
-#ifndef MP3G_FAST_STRAIGHT
-#define MP3G_FAST_STRAIGHT 1
-#endif
-#ifndef MP3G_FAST_NT_STORE
-#define MP3G_FAST_NT_STORE 1  // non-temporal PCM stores: c2 -1.9 %, c3 -0.8 % (tools/gpu_ab.sh)
-#endif
 #ifndef MP3G_FAST_DWIN_STRIDE
 #define MP3G_FAST_DWIN_STRIDE 20
 #endif
@@ -127,7 +123,17 @@ struct __align__(16) WaveSmem {
   // requantization exponents n4 / 4 (float16, exact) of the long bands
   // [ch][sfb] and short bands [ch][sfb][win]
   _Float16 expo[2 * 22 + 2 * 39];
+  // hot-granule zones [start, end) of this chunk, recorded by the fast pass
+  // and redone in the reference's order after it (kHotS)
+  uint32_t zone[8][2];
 };
+constexpr uint32_t kZones = 8;
+
+// The fast kernel's LDS, at namespace scope so that the out-of-line exact
+// zone addresses it as LDS too (no generic pointer to LDS escapes the
+// kernel: those would be 64-bit values in the fast loop's registers).
+__shared__ SharedSmem g_sh;
+__shared__ WaveSmem g_wsm[kWaves];
 
 // Raw coefficients of lane (ch, sb) of granule g: its 18 lines, 36 B at
 // coef[g][ch][18 sb], as 9 dwords (two int16 each) by three 12-B buffer loads
@@ -256,6 +262,626 @@ __device__ __forceinline__ float v_from_x(const float* x, int i) {
   return -x[kSlots * dct32::kPosOfM[i - 48]];
 }
 
+// ---- reference-order fallback for hot granules ------------------------------
+// The reassociated transforms err in proportion to the magnitudes they sum,
+// while the reference's own float32 rounding is reproduced only by its own
+// operation order.  A granule whose hybrid output S (what the matrixing
+// reads) exceeds kHotS in any line of either channel is "hot": its PCM and
+// that of the next granule (whose window reads its V blocks) are computed in
+// the reference's order after the chunk's fast pass (the hot zones), from
+// entry state that is itself exact: a zone replays the granules that state
+// depends on from its replay start (the chunk-halo rule: S_g needs x_{g-1}'s
+// overlap, V_{g-1} needs x_{g-2}'s).
+// Below kHotS the fast transforms stay within +-1 LSB with a 4-8x margin in
+// magnitude (tools/fast_tolerance.py, DESIGN.md "Fast mode on every valid input").
+#ifndef MP3G_HOT_S
+#define MP3G_HOT_S 8.0f
+#endif
+constexpr float kHotS = MP3G_HOT_S;
+#ifndef MP3G_HOT_CHECK
+#define MP3G_HOT_CHECK 1  // 0: timing experiments only (no hot zones: +-1 LSB not guaranteed)
+#endif
+
+// one rounding per operation in the order written: these helpers (and the
+// *_exact functions) are compiled with contraction off
+__device__ __forceinline__ float rmul(float a, float b) {
+#pragma clang fp contract(off)
+  return a * b;
+}
+__device__ __forceinline__ float radd(float a, float b) {
+#pragma clang fp contract(off)
+  return a + b;
+}
+__device__ __forceinline__ float rsub(float a, float b) {
+#pragma clang fp contract(off)
+  return a - b;
+}
+
+// float32(pow(2, n4 / 4) * powtab34[|x|]) with sign (frame.go:148-155,
+// :166-173): the proven table form ldexp(req[n4 & 3][|x|], n4 >> 2)
+// (dsp_tables.h, tests/test_tables.py); e = n4 / 4 exactly in float16
+__device__ __forceinline__ float requant_exact(int xi, _Float16 e) {
+  const int n4 = (int)((float)e * 4.0f);
+  const float v = __builtin_ldexpf(g_req[n4 & 3][min(abs(xi), 8206)], n4 >> 2);
+  return xi < 0 ? -v : v;
+}
+
+// The exact path's tables through a base pointer the compiler cannot prove
+// loop-invariant: scalar loads issued where they are used, not hoisted out
+// of the zone loop as hundreds of live SGPRs.
+__device__ __forceinline__ const float* vtab(const float* p) {
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
+// max |v| over the lane's 18 values (v_max3 with abs modifiers)
+__device__ __forceinline__ float max_abs18(const float* v) {
+  float m = 0.0f;
+#pragma unroll
+  for (int j = 0; j < 18; j++) m = fmaxf(m, fabsf(v[j]));
+  return m;
+}
+
+// imdct.Win + overlap-add + frequency inversion of subband k in the
+// reference's order (imdct.go:83-108, frame.go:454-486): every sum from 0.0
+// over m ascending, product and sum rounded separately.  stp holds the
+// overlap with the frequency-inversion signs folded in (see the kernel);
+// negation commutes with rounding, so folding the sign is exact.
+__device__ __forceinline__ void imdct_exact(const float x[18], int bt, int k, bool act, f2 stp[9], float o[18]) {
+#pragma clang fp contract(off)
+  const float sodd = (k & 1) ? -1.0f : 1.0f;
+  const float* c12 = vtab(&g_fast.cos12[0][0]);
+  const float* c36 = vtab(&g_fast.c36[0][0]);
+  const float* win = vtab(&g_fast.win[0][0]) + 36 * bt;
+  float st[18];
+#pragma unroll
+  for (int q = 0; q < 9; q++) {
+    st[q] = stp[q].x;
+    st[17 - q] = stp[q].y;
+  }
+  if (bt == 2) {
+    // out[6 wi + p + 6] += (sum_m in[wi + 3m] cosN12[m][p]) win[2][p], wi ascending
+#pragma unroll
+    for (int pos = 0; pos < 36; pos++) {
+      float raw = 0.0f;
+#pragma unroll
+      for (int wi = 0; wi < 3; wi++) {
+        const int p = pos - 6 - 6 * wi;
+        if (p < 0 || p >= 12) continue;
+        float sum = 0.0f;
+#pragma unroll
+        for (int m = 0; m < 6; m++) sum = sum + x[wi + 3 * m] * c12[12 * m + p];
+        raw = raw + sum * win[p];
+      }
+      const float f = (pos & 1) ? raw * sodd : raw;
+      if (pos < 18) o[pos] = f + st[pos];
+      else if (act) st[pos - 18] = f;
+    }
+  } else {
+    // the 18 distinct columns of cosN36 (DspTables::cos36_distinct):
+    // col(17 - p) = -col(p), col(53 - p) = col(p) bit for bit
+    float d[18];
+#pragma unroll
+    for (int q = 0; q < 18; q++) {
+      float s = 0.0f;
+#pragma unroll
+      for (int m = 0; m < 18; m++) s = s + x[m] * c36[18 * m + q];
+      d[q] = s;
+    }
+#pragma unroll
+    for (int pos = 0; pos < 36; pos++) {
+      const float v = pos < 9 ? d[pos] : pos < 18 ? -d[17 - pos] : pos < 27 ? d[pos - 9] : d[44 - pos];
+      const float raw = v * win[pos];
+      const float f = (pos & 1) ? raw * sodd : raw;
+      if (pos < 18) o[pos] = f + st[pos];
+      else if (act) st[pos - 18] = f;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 9; q++) stp[q] = (f2){st[q], st[17 - q]};
+}
+
+// V = synthNWin * S of one time slot in the reference's order
+// (frame.go:642-648), as its 32 distinct values X (in place in the ring
+// column slot `colu`: S[j] at colu[kSlots j], X[m] to colu[kSlots kPosOfM[m]]).
+__device__ __forceinline__ void matrix_exact(float* colu) {
+#pragma clang fp contract(off)
+  float S[32];
+#pragma unroll
+  for (int j = 0; j < 32; j++) S[j] = colu[kSlots * j];
+  for (int m = 0; m < 32; m++) {
+    const float* row = vtab(&g_fast.nrow[m][0]);
+    float s = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 32; j++) s = s + row[j] * S[j];
+    colu[kSlots * dct32::kPosOfM[m]] = s;
+  }
+}
+
+// The 16-tap window of output i = k for the 18 slots of a granule in the
+// reference's order (frame.go:649-669): U *= D rounded, summed j = 0..15
+// from 0.0, times 32767 rounded; acc2[p] = slots (2p, 2p + 1) as in the fast
+// window (RA / RB: the X columns of V_j[i], j even, and V_j[32 + i], j odd;
+// the V -> X signs are folded into FastTables::dwin, exactly).  V[16] (the
+// reference's ~1e-16 |S| residue of a zero row) is taken as 0.
+__device__ __forceinline__ void window_exact(const float* RA, const float* RB, int k, f2 acc2[9]) {
+#pragma clang fp contract(off)
+  float dw[16];
+#pragma unroll
+  for (int j = 0; j < 16; j++) dw[j] = vtab(&g_fast.dwin[0][0])[16 * k + j];
+#pragma unroll
+  for (int ss = 0; ss < 18; ss++) {
+    float sum = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 16; j++) sum = sum + ((j & 1) ? RB : RA)[kHist + ss - j] * dw[j];
+    const float t = sum * 32767.0f;
+    if (ss & 1) acc2[ss >> 1].y = t;
+    else acc2[ss >> 1].x = t;
+  }
+}
+
+// ---- per-granule stages shared by the fast loop and the exact zone ----------
+__device__ __forceinline__ bool is_short_blk(uint32_t d1) { return (d1 & 0x00ffff00u) == 0x00020100u; }
+
+// The granule's wave-uniform parameters (SGPRs) and this lane's channel's.
+struct GranParams {
+  uint32_t h;
+  int nch, combo;
+  // the channels' scalar parameters (one 8-B LDS read each):
+  // cp0 = count1 | global_gain << 16 | scalefac_scale << 24,
+  // cp1 = preflag | win_switch_flag << 8 | block_type << 16 | mixed_block_flag << 24
+  uint32_t cp0[2], cp1[2];
+  bool all_long;  // every channel of this granule is a long block (no reorder)
+  // this lane's channel (lanes of an absent channel mirror channel 0's block
+  // layout: no extra divergence)
+  uint32_t d1;
+  int count1;
+  bool shortblk, mixed;
+};
+
+// Reads the descriptor in s.desc and fills the band exponents s.expo (long
+// bands only when no channel has short blocks).
+__device__ __forceinline__ GranParams granule_params(WaveSmem& s, int ch) {
+  GranParams P;
+  // wave-uniform (SGPR): the per-combo tables become scalar loads
+  P.h = __builtin_amdgcn_readfirstlane(s.desc.header);
+  P.nch = hdr_nch(P.h);
+  P.combo = hdr_combo(P.h);
+#pragma unroll
+  for (int c = 0; c < 2; c++) {
+    const uint2 v = *reinterpret_cast<const uint2*>(&s.desc.ch[c]);
+    P.cp0[c] = __builtin_amdgcn_readfirstlane(v.x);
+    P.cp1[c] = __builtin_amdgcn_readfirstlane(v.y);
+  }
+  P.all_long = !is_short_blk(P.cp1[0]) && (P.nch == 1 || !is_short_blk(P.cp1[1]));
+  const bool act = ch < P.nch;
+  const uint32_t d0 = (act && ch) ? P.cp0[1] : P.cp0[0];
+  P.d1 = (act && ch) ? P.cp1[1] : P.cp1[0];
+  {
+    // long bands: lane = (c, sfb), 44 lanes
+    const int e = lane_fresh();
+    if (e < 44) {
+      const int c = e >= 22, sfb = e - 22 * c;
+      const uint32_t a0 = c ? P.cp0[1] : P.cp0[0], a1 = c ? P.cp1[1] : P.cp1[0];
+      const int v = (int)((a0 >> 16) & 0xffu) - 210 -
+                    ((a0 >> 24) ? 4 : 2) * ((int)s.desc.ch[c].scalefac_l[sfb] + (int)(a1 & 0xffu) * kPretab(sfb));
+      s.expo[e] = (_Float16)(0.25f * (float)v);
+    }
+    if (!P.all_long) {
+      // short bands: (c, sfb, win), 78 entries
+      for (int r0 = e; r0 < 2 * 39; r0 += kLanes) {
+        const int c = r0 >= 39, r = r0 - 39 * c, sfb = r / 3, win = r - 3 * sfb;
+        const uint32_t a0 = c ? P.cp0[1] : P.cp0[0];
+        const mp3g_channel& D = s.desc.ch[c];
+        const int v = (int)((a0 >> 16) & 0xffu) - 210 - 8 * (int)D.subblock_gain[win] -
+                      ((a0 >> 24) ? 4 : 2) * (int)D.scalefac_s[sfb][win];
+        s.expo[44 + r0] = (_Float16)(0.25f * (float)v);
+      }
+    }
+  }
+  P.count1 = (int)(d0 & 0xffffu);
+  P.shortblk = is_short_blk(P.d1);
+  P.mixed = (P.d1 >> 24) != 0;
+  wave_sync();
+  return P;
+}
+
+// Requantization of long-block granules, lane = (ch, sb = k), from the raw
+// lines in registers.
+__device__ __forceinline__ void front_long_fast(float x[18], const uint32_t cw[9], const WaveSmem& s,
+                                                const SharedSmem& sh, const GranParams& P, int ch, int k) {
+  int xi[18];
+#pragma unroll
+  for (int q = 0; q < 9; q++) {
+    xi[2 * q] = (int)(int16_t)(cw[q] & 0xffffu);
+    xi[2 * q + 1] = (int)(int16_t)(cw[q] >> 16);
+  }
+  // long band of line j: first band of the subband + band starts among
+  // lines 1..j.  Every long band starts at an even line (consts.go:68-97
+  // SfBandIndices; dsp_tables.cpp checks it), so lines 2q and 2q + 1
+  // share one band: one exponent read per line pair.
+  const uint32_t lb = sh.lband[P.combo][k];
+  _Float16 ex[9];
+#pragma unroll
+  for (int q = 0; q < 9; q++)
+    ex[q] = s.expo[22 * ch + (int)(lb & 31u) + __builtin_popcount((lb >> 5) & ((2u << (2 * q)) - 1u))];
+  // Lines >= count1 hold zeros (the bitstream parse's guarantee,
+  // maindata/huffman.go:130-134; mp3g_validate checks it), and requantizing
+  // 0 gives 0, so long blocks need no per-line count1 test here.
+  // (absent-channel lanes compute garbage that nothing reads)
+#pragma unroll
+  for (int j = 0; j < 18; j++) x[j] = requant_fast(xi[j], ex[j >> 1]);
+}
+
+// Requantization in gather form (any block type; the reorder of short
+// blocks, frame.go:184-302): the channel's raw lines staged in the current
+// slots of the ring, lane (ch, sb) gathering its 18 output lines.
+template <bool kExact>
+__device__ __forceinline__ void front_gather(float x[18], const uint32_t cw[9], WaveSmem& s, const GranParams& P,
+                                             int ch, int k) {
+  int nsfs = 0;  // short bands whose first line lies below count1 (frame.go:229-255 loop bound)
+#pragma unroll
+  for (int b = 0; b < 13; b++) nsfs += 3 * (int)g_fast.sfb_short[P.combo][b] < P.count1;
+  {
+    uint32_t* col = reinterpret_cast<uint32_t*>(&s.ring[ch][k][kHist]);
+#pragma unroll
+    for (int q = 0; q < 9; q++) col[q] = cw[q];
+  }
+  wave_sync();
+  const int16_t* rch = reinterpret_cast<const int16_t*>(&s.ring[ch][0][kHist]);
+  // line info through a buffer resource (SGPR base, 32-bit lane offset) and
+  // the lane's first line recomputed here: nothing of this rare path stays
+  // live (in VGPRs) across the granule loop
+  const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint32_t*>(&g_fast.linfo[P.combo][0]), (short)0, 576 * 4, 0x00020000);
+  const int L0 = 18 * (lane_fresh() & 31);
+#pragma unroll
+  for (int j = 0; j < 18; j++) {
+    const int L = L0 + j;
+    const uint32_t inf = __builtin_amdgcn_raw_buffer_load_b32(rl, 4 * L, 0, 0);
+    const int sfl = inf & 31, sfs = (inf >> 5) & 15, wsrc = (inf >> 9) & 3, wown = (inf >> 11) & 3;
+    const int srcr = inf >> 13;
+    const bool longlike = !P.shortblk || (P.mixed && L < 36);
+    const bool started = sfs < nsfs;
+    const bool reord = sfs == (P.mixed ? 3 : 0) || started;
+    const int src = seli(longlike || !reord, L, srcr);
+    const int win = seli(reord, wsrc, wown);
+    const int eidx = seli(longlike, 22 * ch + sfl, 44 + 39 * ch + 3 * sfs + win);
+    const bool process = longlike ? (P.shortblk || L < P.count1) : started;
+    const int sk = (src * 3641) >> 16;  // src / 18 for src < 576
+    const int xi = rch[2 * kSlots * sk + (src - 18 * sk)];
+    const float v = kExact ? requant_exact(xi, s.expo[eidx]) : requant_fast(xi, s.expo[eidx]);
+    x[j] = self(process, v, (float)xi);
+  }
+  wave_sync();  // staged lines read before the slots are reused
+}
+
+// MS / intensity stereo with the partner channel's lane (frame.go:304-420):
+// single roundings in the reference's order, exact in both modes.
+__device__ __forceinline__ void stereo_stage(float x[18], const WaveSmem& s, const SharedSmem& sh,
+                                             const GranParams& P, int ch) {
+  if (!(P.nch == 2 && hdr_mode(P.h) == 1 && (P.h & 0x30u))) return;
+  const mp3g_channel& C0 = s.desc.ch[0];
+  const int c1r = (int)(P.cp0[1] & 0xffffu);
+  const int msmax = max((int)(P.cp0[0] & 0xffffu), c1r);
+  const bool ms = P.h & 0x20u, is = P.h & 0x10u;
+  const bool short0 = is_short_blk(P.cp1[0]);
+  const bool mixed0 = (P.cp1[0] >> 24) != 0;
+  const float inv_sqrt2 = 0.70710678118654752440f;
+  if (ms) {
+    // MS: L' = (l + r)c, R' = (l - r)c for lines below max(count1)
+    // (frame.go:362-377).  Two lines per step: one swap gives lanes < 32
+    // (l, r) of line j and lanes >= 32 those of line j + 1, (l + r)c,
+    // (l - r)c in one packed pair, a second swap hands back L' / R' of
+    // both lines to their channels' lanes.  Long blocks without intensity
+    // stereo transform every line: at or above max(count1) both channels
+    // are 0, where (l +- r)c is 0 too.  Otherwise lines >= max(count1) keep
+    // their values (the reorder can move values past count1; IS follows).
+    auto ms_pair = [&](float& u, float& v) {
+      const auto r = __builtin_amdgcn_permlane32_swap(__float_as_int(u), __float_as_int(v), false, false);
+      const float a = __int_as_float(r[0]), b = __int_as_float(r[1]);
+      const f2 pq = (f2){a + b, a - b} * bcast(inv_sqrt2);
+      const auto r2 = __builtin_amdgcn_permlane32_swap(__float_as_int(pq.x), __float_as_int(pq.y), false, false);
+      u = __int_as_float(r2[0]);
+      v = __int_as_float(r2[1]);
+    };
+    if (P.all_long && !is) {  // wave-uniform
+#pragma unroll
+      for (int j = 0; j < 18; j += 2) ms_pair(x[j], x[j + 1]);
+    } else {
+      const int left = msmax - 18 * (lane_fresh() & 31);  // lines of this subband below msmax
+#pragma unroll
+      for (int j = 0; j < 18; j += 2) {
+        float n0 = x[j], n1 = x[j + 1];
+        ms_pair(n0, n1);
+        x[j] = j < left ? n0 : x[j];
+        x[j + 1] = j + 1 < left ? n1 : x[j + 1];
+      }
+    }
+  }
+  if (is) {
+    // Intensity stereo per line of this lane (frame.go:308-359, :379-419):
+    // bands at or above channel 1's count1, ratio index from CHANNEL 0's
+    // scale factors, each channel scaled by its own ratio (is_pos 7 = no
+    // change: isr[7] = (1, 1)).  Long blocks: the line's band from the
+    // subband's band-start mask (as in the requantization); short / mixed
+    // blocks: the line info table.
+    const int k0 = lane_fresh() & 31;
+    int nl_is = 0, ns_is = 0;  // first long / short band starting at or above channel 1's count1
+#pragma unroll
+    for (int b = 0; b < 23; b++) nl_is += (int)g_fast.sfb_long[P.combo][b] < c1r;
+#pragma unroll
+    for (int b = 0; b < 14; b++) ns_is += 3 * (int)g_fast.sfb_short[P.combo][b] < c1r;
+    if (!short0) {
+      const uint32_t lb = sh.lband[P.combo][k0];
+#pragma unroll
+      for (int j = 0; j < 18; j++) {
+        const int sfl = (int)(lb & 31u) + __builtin_popcount((lb >> 5) & ((2u << j) - 1u));
+        const int pos = min((int)C0.scalefac_l[min(sfl, 21)], 7);
+        const float rr = sh.isr[pos][ch];
+        x[j] = (sfl < 21 && sfl >= nl_is) ? x[j] * rr : x[j];
+      }
+    } else {
+      const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<uint32_t*>(&g_fast.linfo[P.combo][0]), (short)0, 576 * 4, 0x00020000);
+#pragma unroll
+      for (int j = 0; j < 18; j++) {
+        const uint32_t info = __builtin_amdgcn_raw_buffer_load_b32(rl, 4 * (18 * k0 + j), 0, 0);
+        const int sfl = info & 31, sfs = (info >> 5) & 15, wown = (info >> 11) & 3;
+        const bool lp = mixed0 && sfl < 8 && sfl >= nl_is;
+        const bool sp = sfs < 12 && (!mixed0 || sfs >= 3) && sfs >= ns_is;
+        const int pl = lp ? min((int)C0.scalefac_l[min(sfl, 21)], 7) : 7;
+        const int ps = sp ? min((int)C0.scalefac_s[min(sfs, 12)][min(wown, 2)], 7) : 7;
+        x[j] = x[j] * sh.isr[pl][ch] * sh.isr[ps][ch];
+      }
+    }
+  }
+}
+
+// Antialias butterflies with the neighbouring subbands' lanes (DPP wave
+// shifts; frame.go:427-452).  kExact: the reference's two products and one
+// sum per output, each rounded.
+template <bool kExact>
+__device__ __forceinline__ void antialias_stage(float x[18], const GranParams& P, bool act, int k) {
+  const bool sw = P.shortblk;
+  const bool skip = !act || (sw && !P.mixed);
+  const int sblim = (sw && P.mixed) ? 2 : 32;
+  const bool lower = !skip && k >= 1 && k < sblim;     // butterfly with subband k-1
+  const bool upper = !skip && k < 31 && k + 1 < sblim;  // butterfly with subband k+1
+  float up[8], dn[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    up[i] = xl::from_prev(x[17 - i]);  // x_{k-1}[17-i]
+    dn[i] = xl::from_next(x[i]);       // x_{k+1}[i]
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const float cs = g_fast.aa_cs[i], ca = g_fast.aa_ca[i];  // (16 SGPRs, as in the fast loop)
+    const float ui = x[i], li = x[17 - i];
+    if (kExact) {
+      x[i] = self(lower, radd(rmul(ui, cs), rmul(up[i], ca)), ui);
+      x[17 - i] = self(upper, rsub(rmul(li, cs), rmul(dn[i], ca)), li);
+    } else {
+      x[i] = self(lower, ui * cs + up[i] * ca, ui);
+      x[17 - i] = self(upper, li * cs - dn[i] * ca, li);
+    }
+  }
+}
+
+// Block type of subband k's IMDCT: long windows for subbands 0, 1 whenever
+// win_switch && mixed (frame.go:462-466)
+__device__ __forceinline__ int imdct_block_type(uint32_t d1, int k) {
+  int bt = (int)((d1 >> 16) & 3u);
+  if ((d1 & 0xff00ff00u) == 0x01000100u && k < 2) bt = 0;
+  return bt;
+}
+
+// IMDCT + overlap + frequency inversion in fast order: raw[0..17] + old
+// overlap -> o[], raw[18..35] -> new overlap, frequency inversion riding on
+// the signs of the windows and of stp.
+__device__ __forceinline__ void imdct_fast(const float x[18], int bt, int nch, bool act, float sodd,
+                                           const SharedSmem& sh, f2 stp[9], float o[18]) {
+  if (bt == 2) {
+    float st[18];
+#pragma unroll
+    for (int q = 0; q < 9; q++) {
+      st[q] = stp[q].x;
+      st[17 - q] = stp[q].y;
+    }
+    // raw[pos] = sum over the windows wi with 0 <= pos-6-6wi < 12 of
+    // (sum_m x[wi+3m] cosN12[m][p]) * win[2][p], p = pos-6-6wi (imdct.go:88-94)
+#pragma unroll
+    for (int pos = 0; pos < 36; pos++) {
+      float raw = 0.0f;
+#pragma unroll
+      for (int wi = 0; wi < 3; wi++) {
+        const int p = pos - 6 - 6 * wi;
+        if (p < 0 || p >= 12) continue;
+        float sum = 0.0f;
+#pragma unroll
+        for (int m = 0; m < 6; m++) sum += x[wi + 3 * m] * dct4::kCos12[p][m];
+        raw += sum * dct4::kWin12[p];
+      }
+      if (pos & 1) raw *= sodd;  // (pos and pos - 18 have the same parity)
+      if (pos < 18) o[pos] = raw + st[pos];
+      else st[pos - 18] = self(act, raw, st[pos - 18]);
+    }
+#pragma unroll
+    for (int q = 0; q < 9; q++) stp[q] = (f2){st[q], st[17 - q]};
+  } else {
+    // the 18 distinct sums are a DCT-IV of size 18 (dct4_18.h):
+    // sum_m x[m] cosN36[m][q] = X[9+q], sum_m x[m] cosN36[m][18+q] = -X[8-q];
+    // packed, pair k = (X[2k], X[17-2k]) holds X[9+q] and X[8-q] of one q
+    f2 P[9];
+    dct4::dct4_18_pk(x, P);
+    const float4* Wq = sh.winp[bt][lane_fresh() & 1];
+    // (the overlap of an absent channel stays frozen: frame.go Decode
+    // touches ch < nch only; stereo granules need no per-lane select)
+    auto overlap = [&](auto frozen) {
+#pragma unroll
+      for (int kk = 0; kk < 9; kk++) {
+        const int q = kk <= 4 ? 8 - 2 * kk : 2 * kk - 9;
+        const float za = kk <= 4 ? P[kk].y : P[kk].x;  // X[9+q]
+        const float zb = kk <= 4 ? P[kk].x : P[kk].y;  // X[8-q]
+        const float4 w = Wq[q];
+        // (o[q], o[17-q]) = X[9+q] (W[q], -W[17-q]) + stp[q];
+        // new stp[q] = X[8-q] (-W[18+q], -W[35-q])   (signs folded in w)
+        const f2 oq = pfma(bcast(za), (f2){w.x, w.y}, stp[q]);
+        o[q] = oq.x;
+        o[17 - q] = oq.y;
+        const f2 ns = bcast(zb) * (f2){w.z, w.w};
+        if constexpr (decltype(frozen)::value)
+          stp[q] = (f2){self(act, ns.x, stp[q].x), self(act, ns.y, stp[q].y)};
+        else
+          stp[q] = ns;
+      }
+    };
+    if (nch == 2) overlap(std::false_type{});
+    else overlap(std::true_type{});
+  }
+}
+
+// (L, R) sample pairs without LDS staging: one v_permlane32_swap per slot
+// pair hands lane i slot 2p's (L, R) and lane 32 + i slot 2p + 1's, so every
+// lane stores one dword per slot pair and the wave 2 x 128 contiguous bytes.
+// Mono: the swap hands lane i channel 0's slot 2p and lane 32 + i its slot
+// 2p + 1, stored in both halves (frame.go:671-678).  acc2 holds sum * 32767.
+__device__ __forceinline__ void pack_pcm(const f2 acc2[9], int nch, uint32_t pk[9]) {
+  auto pack = [&](auto mono) {
+#pragma unroll
+    for (int p = 0; p < 9; p++) {
+      // int(sum * 32767) clamped to +-32767 (frame.go:663-669); no decodable
+      // input gets near NaN or |t| >= 2^63 (|sum| < 1e12)
+      const int a = (int)__builtin_amdgcn_fmed3f(acc2[p].x, -32767.0f, 32767.0f);
+      const int b = (int)__builtin_amdgcn_fmed3f(acc2[p].y, -32767.0f, 32767.0f);
+      const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+      // low halves of (r[0], r[1]) -> one dword: L | R << 16 (R = L for mono)
+      pk[p] = __builtin_amdgcn_perm((uint32_t)(decltype(mono)::value ? r[0] : r[1]), (uint32_t)r[0], 0x05040100u);
+    }
+  };
+  if (nch == 2) pack(std::false_type{});
+  else pack(std::true_type{});
+}
+
+// PCM of granule g: one dword per lane and slot pair, non-temporal (c2
+// -1.9 %, c3 -0.8 %).  Issued for replayed granules too, through a resource
+// with no records (straight-line vmcnt accounting).
+__device__ __forceinline__ void store_pcm(int16_t* pcm, uint32_t g, bool out, const uint32_t pk[9], int hi, int k) {
+  const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
+      pcm + (size_t)g * 1152, (short)0, out ? MP3G_PCM_BYTES_PER_GRANULE : 0, 0x00020000);
+#pragma unroll
+  for (int p = 0; p < 9; p++) __builtin_amdgcn_raw_buffer_store_b32(pk[p], rp, 4 * (32 * (2 * p + hi) + k), 0, 2);
+}
+
+// Entry state of a replay start: overlap store in registers, V history as X
+// vectors, from the stream's state_in (init_in) or zero.  stp[q] =
+// (store[q], store[17-q]), each element times the frequency-inversion sign of
+// its line (odd line of an odd subband: -1), so the overlap-add yields
+// frequency-inverted output directly.
+__device__ __forceinline__ void init_state(WaveSmem& s, const mp3g_state* sin, const int init_in[2], int lane,
+                                           f2 stp[9]) {
+  const int ch = lane >> 5, k = lane & 31;
+  const float sodd = (k & 1) ? -1.0f : 1.0f;
+  // (no dynamic indexing of init_in[]: a private array would be promoted to LDS)
+  const bool in0 = init_in[0] && sin, in1 = init_in[1] && sin;
+  const bool from_in = ch ? in1 : in0;
+#pragma unroll
+  for (int q = 0; q < 9; q++) {
+    const float a = from_in ? sin->store[ch][k][q] : 0.0f, b = from_in ? sin->store[ch][k][17 - q] : 0.0f;
+    stp[q] = (f2){(q & 1) ? a * sodd : a, (q & 1) ? b : b * sodd};
+  }
+  for (int e = lane; e < 2 * 15 * 32; e += kLanes) {
+    const int c = e / (15 * 32), blk = (e >> 5) % 15, m = e & 31;
+    const bool in = c ? in1 : in0;
+    s.ring[c][dct32::kPosOfM[m]][kHist - 1 - blk] = in ? x_from_v(&sin->vvec[c][64 * blk], m) : 0.0f;
+  }
+}
+
+// The granule's descriptor into s.desc and its lines into cw (direct loads).
+__device__ __forceinline__ void load_granule(const mp3g_granule* gran, const int16_t* coef, uint32_t g, int lane,
+                                             WaveSmem& s, uint32_t cw[9]) {
+  load_lines(coef, g, lane, cw);
+  if (lane < 10) reinterpret_cast<uint4*>(&s.desc)[lane] = reinterpret_cast<const uint4*>(gran + g)[lane];
+}
+
+// Does replayed granule g (< out_from) produce V a later granule reads? Only
+// the last replayed one, or one followed by a granule with fewer channels
+// (see v2 / DESIGN.md halo).
+__device__ __forceinline__ bool replay_needs_v(const mp3g_granule* gran, uint32_t g, uint32_t out_from,
+                                               const WaveSmem& s) {
+  if (g >= out_from || g + 1 >= out_from) return true;
+  return hdr_nch(gran[g + 1].header) < hdr_nch(s.desc.header);
+}
+
+// One granule in the reference's operation order (the hot-zone fixup):
+// descriptor and lines loaded directly, every stage exact, PCM stored when
+// `out`.  Returns whether the granule is hot by its exact hybrid output.
+__device__ __forceinline__ bool exact_granule(const mp3g_granule* __restrict__ gran, const int16_t* __restrict__ coef,
+                                              int16_t* __restrict__ pcm, WaveSmem& s, const SharedSmem& sh,
+                                              uint32_t g, bool out, bool need_v, f2 stp[9]) {
+  const int lane = lane_fresh();
+  const int ch = lane >> 5, k = lane & 31, hi = lane >> 5;
+  uint32_t cw[9];
+  load_granule(gran, coef, g, lane, s, cw);
+  wave_sync();
+  const GranParams P = granule_params(s, ch);
+  const bool act = ch < P.nch;
+  float x[18];
+  front_gather<true>(x, cw, s, P, ch, k);
+  stereo_stage(x, s, sh, P, ch);
+  antialias_stage<true>(x, P, act, k);
+  float o[18];
+  imdct_exact(x, imdct_block_type(P.d1, k), k, act, stp, o);
+  const bool hot = __builtin_amdgcn_ballot_w64((act ? max_abs18(o) : 0.0f) > kHotS) != 0;
+  if (need_v && act) {
+#pragma unroll
+    for (int j = 0; j < 18; j++) s.ring[ch][k][kHist + j] = o[j];
+  }
+  wave_sync();
+  if (need_v && act && (lane & 31) < 18) matrix_exact(&s.ring[ch][0][kHist + (lane & 31)]);
+  wave_sync();
+  uint32_t pk[9] = {};
+  if (out) {
+    const int pa = dct32::kPosOfM[k < 16 ? 16 + k : (k == 16 ? 0 : 48 - k)];
+    const int pb = dct32::kPosOfM[k < 16 ? 16 - k : k - 16];
+    f2 acc2[9];
+    window_exact(&s.ring[ch][pa][0], &s.ring[ch][pb][0], k, acc2);
+    pack_pcm(acc2, P.nch, pk);
+  }
+  store_pcm(pcm, g, out, pk, hi, k);
+  wave_sync();
+  if (ch < P.nch && need_v) {
+    f2* col = reinterpret_cast<f2*>(&s.ring[ch][k][0]);
+#pragma unroll
+    for (int q = 0; q < 8; q++) col[q] = col[9 + q];
+  }
+  wave_sync();
+  return hot;
+}
+
+// Zones recorded by the fast pass (WaveSmem::zone): a hot granule g opens
+// (or extends) the zone [max(g, out_first), g + 2) of granules whose PCM
+// depends on its hybrid output (the window of g + 1 reads g's V blocks).
+// When the list is full the last zone runs to the chunk end.
+template <class Smem>
+__device__ __forceinline__ void record_hot(Smem& s, uint32_t& nz, uint32_t g, uint32_t out_first, uint32_t end) {
+  const uint32_t zs = g > out_first ? g : out_first, ze = g + 2 < end ? g + 2 : end;
+  if (zs >= ze) return;  // a replayed granule whose V no output reads
+  const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  if (nz > 0 && zs <= s.zone[nz - 1][1]) {
+    if (lane == 0) s.zone[nz - 1][1] = ze > s.zone[nz - 1][1] ? ze : s.zone[nz - 1][1];
+  } else if (nz < kZones) {
+    if (lane == 0) {
+      s.zone[nz][0] = zs;
+      s.zone[nz][1] = ze;
+    }
+    nz++;
+  } else if (lane == 0) {
+    s.zone[kZones - 1][1] = end;
+  }
+  wave_sync();
+}
+
 }  // namespace
 
 // kStamp: diagnostic build -- per-phase s_memtime cycle sums of every wave go
@@ -276,14 +902,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       tprev = t;
     }
   };
-  __shared__ SharedSmem sh;
-  __shared__ WaveSmem wsm[kWaves];
-#ifdef MP3G_FAST_LDS_PAD
-  // diagnostic builds only (tools/build_variant.sh): extra LDS per workgroup
-  // to lower the resident workgroups per CU (occupancy sensitivity)
-  __shared__ char ldspad[MP3G_FAST_LDS_PAD];
-  if (n_chunks == 0xffffffffu) reinterpret_cast<volatile char*>(ldspad)[threadIdx.x] = 0;
-#endif
+  SharedSmem& sh = g_sh;
   {
     const int t = threadIdx.x;
     for (int e = t; e < 4 * 2 * 9; e += kLanes * kWaves) {
@@ -304,7 +923,8 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
   // loads and its fields (pointers, counts) stay out of the VGPR budget
   const uint32_t ci = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + (threadIdx.x >> 6));
   if (ci >= n_chunks) return;
-  WaveSmem& s = wsm[threadIdx.x >> 6];
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  WaveSmem& s = g_wsm[wave];
   const ChunkDesc cd = chunks[ci];
   const int ch = lane >> 5, k = lane & 31;
   // ring positions of the two X values the window of output i = k reads
@@ -317,48 +937,22 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
   // loop state as wave-uniform 32-bit scalars (plans are limited to < 2^32
   // granules): keeps it in SGPRs, so per-granule header reads are scalar loads
   // (lgkmcnt) that never wait behind the prefetch loads or PCM stores (vmcnt)
-#ifdef MP3G_EXP_NOHALO
-  const uint32_t w = __builtin_amdgcn_readfirstlane((uint32_t)cd.out_first);  // timing experiment only: wrong PCM
-#else
   const uint32_t w = __builtin_amdgcn_readfirstlane((uint32_t)w64);
-#endif
   const uint32_t out_first = __builtin_amdgcn_readfirstlane((uint32_t)cd.out_first);
   const uint32_t end = __builtin_amdgcn_readfirstlane((uint32_t)(cd.out_first + cd.n_out));
   const mp3g_state* sin = state_in ? state_in + cd.stream : nullptr;
-
-  // entry state: overlap store in registers, V history as X vectors
-  // IMDCT overlap `store` (frame.go:473-476) in registers as pairs
-  // stp[q] = (store[q], store[17-q]), each element times the frequency-inversion
-  // sign of its line (odd line of an odd subband: -1), so the overlap-add
-  // yields frequency-inverted output directly
   const float sodd = (k & 1) ? -1.0f : 1.0f;  // sign of the odd lines of this subband
   f2 stp[9];
-  {
-    // (no dynamic indexing of init_in[]: a private array would be promoted to LDS)
-    const bool in0 = init_in[0] && sin, in1 = init_in[1] && sin;
-    const bool from_in = ch ? in1 : in0;
-#pragma unroll
-    for (int q = 0; q < 9; q++) {
-      const float a = from_in ? sin->store[ch][k][q] : 0.0f, b = from_in ? sin->store[ch][k][17 - q] : 0.0f;
-      stp[q] = (f2){(q & 1) ? a * sodd : a, (q & 1) ? b : b * sodd};
-    }
-    for (int e = lane; e < 2 * 15 * 32; e += kLanes) {
-      const int c = e / (15 * 32), blk = (e >> 5) % 15, m = e & 31;
-      const bool in = c ? in1 : in0;
-      s.ring[c][dct32::kPosOfM[m]][kHist - 1 - blk] = in ? x_from_v(&sin->vvec[c][64 * blk], m) : 0.0f;
-    }
-  }
+  init_state(s, sin, init_in, lane, stp);
 
   uint32_t cw[9] = {};  // the current granule's raw coefficients (lane's 18 lines)
-  if (w < end) {
-    load_lines(coef, w, lane, cw);
-    if (lane < 10) reinterpret_cast<uint4*>(&s.desc)[lane] = reinterpret_cast<const uint4*>(gran + w)[lane];
-  }
+  if (w < end) load_granule(gran, coef, w, lane, s, cw);
   wave_sync();
 
-  // PCM of a granule: one dword (L, R) per lane and slot pair
-  uint32_t pk[9] = {};
   const int hi = lane >> 5;
+  // PCM of a granule: one dword (L, R) per lane and slot pair (a replayed
+  // granule stores stale values to a resource with no records)
+  uint32_t pk[9] = {};
 
   if constexpr (kStamp) {
     tprev = __builtin_amdgcn_s_memtime();
@@ -371,505 +965,204 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
   // 34 .. 101 us for identical chunks).  A wave with more of its chunk left
   // takes a higher priority, which keeps the co-resident waves abreast.
   const uint32_t span = end - w, span2 = 2 * span, span3 = 3 * span;
-  for (uint32_t g = w; g < end; g++) {
-#ifdef MP3G_EXP_SALU
-    // timing experiment only (tools/build_variant.sh): extra scalar ALU work
-    {
-      uint32_t d = g;
-#pragma unroll
-      for (int i = 0; i < MP3G_EXP_SALU; i++) asm volatile("s_add_u32 %0, %0, 1" : "+s"(d));
-    }
-#endif
-#ifndef MP3G_EXP_NOPRIO
-    {
-      const uint32_t left4 = 4u * (end - g);  // priority floor(4 * left / span), 3 .. 0
-      if (left4 > span3) __builtin_amdgcn_s_setprio(3);
-      else if (left4 > span2) __builtin_amdgcn_s_setprio(2);
-      else if (left4 > span) __builtin_amdgcn_s_setprio(1);
-      else __builtin_amdgcn_s_setprio(0);
-    }
-#endif
-    const bool out = g >= out_first;
-    // does a replayed granule's V feed anything? (see v2 / DESIGN.md halo)
-    bool need_v = true;
-    if (!out && g + 1 < out_first) need_v = hdr_nch(gran[g + 1].header) < hdr_nch(s.desc.header);
-    // wave-uniform (SGPR): the per-combo tables below become scalar loads
-    const uint32_t h = __builtin_amdgcn_readfirstlane(s.desc.header);
-    const int nch = hdr_nch(h), combo = hdr_combo(h);
-    const bool act = ch < nch;
-    // the channels' scalar parameters in SGPRs (one 8-B LDS read each):
-    // dword 0 = count1 | global_gain << 16 | scalefac_scale << 24,
-    // dword 1 = preflag | win_switch_flag << 8 | block_type << 16 | mixed_block_flag << 24
-    uint32_t cp0[2], cp1[2];
-#pragma unroll
-    for (int c = 0; c < 2; c++) {
-      const uint2 v = *reinterpret_cast<const uint2*>(&s.desc.ch[c]);
-      cp0[c] = __builtin_amdgcn_readfirstlane(v.x);
-      cp1[c] = __builtin_amdgcn_readfirstlane(v.y);
-    }
-    auto is_short = [](uint32_t d1) { return (d1 & 0x00ffff00u) == 0x00020100u; };  // win_switch 1, block_type 2
-    // wave-uniform: every channel of this granule is a long block (no reorder)
-    const bool all_long = !is_short(cp1[0]) && (nch == 1 || !is_short(cp1[1]));
-    // this lane's channel (lanes of an absent channel mirror channel 0's block
-    // layout: no extra divergence)
-    const uint32_t d0 = (act && ch) ? cp0[1] : cp0[0], d1 = (act && ch) ? cp1[1] : cp1[0];
-
-    // ---- per-granule front-end parameters: band exponents (long bands only
-    //      when no channel has short blocks) ----
-    {
-      // long bands: lane = (c, sfb), 44 lanes
-      const int e = lane_fresh();
-      if (e < 44) {
-        const int c = e >= 22, sfb = e - 22 * c;
-        const uint32_t a0 = c ? cp0[1] : cp0[0], a1 = c ? cp1[1] : cp1[0];
-        const int v = (int)((a0 >> 16) & 0xffu) - 210 -
-                      ((a0 >> 24) ? 4 : 2) * ((int)s.desc.ch[c].scalefac_l[sfb] + (int)(a1 & 0xffu) * kPretab(sfb));
-        s.expo[e] = (_Float16)(0.25f * (float)v);
+  uint32_t nz = 0;  // hot zones recorded (s.zone)
+  {
+    for (uint32_t g = w; g < end; g++) {
+      {
+        const uint32_t left4 = 4u * (end - g);  // priority floor(4 * left / span), 3 .. 0
+        if (left4 > span3) __builtin_amdgcn_s_setprio(3);
+        else if (left4 > span2) __builtin_amdgcn_s_setprio(2);
+        else if (left4 > span) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
       }
-      if (!all_long) {
-        // short bands: (c, sfb, win), 78 entries
-        for (int r0 = e; r0 < 2 * 39; r0 += kLanes) {
-          const int c = r0 >= 39, r = r0 - 39 * c, sfb = r / 3, win = r - 3 * sfb;
-          const uint32_t a0 = c ? cp0[1] : cp0[0];
-          const mp3g_channel& D = s.desc.ch[c];
-          const int v = (int)((a0 >> 16) & 0xffu) - 210 - 8 * (int)D.subblock_gain[win] -
-                        ((a0 >> 24) ? 4 : 2) * (int)D.scalefac_s[sfb][win];
-          s.expo[44 + r0] = (_Float16)(0.25f * (float)v);
+      const bool out = g >= out_first;
+      const bool need_v = replay_needs_v(gran, g, out_first, s);
+      const GranParams P = granule_params(s, ch);
+      const bool act = ch < P.nch;
+      stamp(0);
+
+      // ---- front end: requantize (gather through the reorder), lane = (ch, sb = k) ----
+      float x[18];
+      if (P.all_long) front_long_fast(x, cw, s, sh, P, ch, k);
+      else front_gather<false>(x, cw, s, P, ch, k);
+      stamp(1);
+      stereo_stage(x, s, sh, P, ch);
+      antialias_stage<false>(x, P, act, k);
+      stamp(2);
+
+      // ---- IMDCT + overlap + frequency inversion ----
+      float o[18];
+      imdct_fast(x, imdct_block_type(P.d1, k), P.nch, act, sodd, sh, stp, o);
+      // ---- a hot granule (wave-uniform test): its zone is redone in the
+      //      reference's order after the pass ----
+#if MP3G_HOT_CHECK
+      if (__builtin_amdgcn_ballot_w64((act ? max_abs18(o) : 0.0f) > kHotS)) record_hot(s, nz, g, out_first, end);
+#endif
+      stamp(3);
+      // prefetch the next granule: lands during the matrixing and window phases
+      // (issued here, not at the top, so its 13 VGPRs are not live across the
+      // front end and IMDCT); buffer resources with SGPR bases and 32-bit lane
+      // offsets: no 64-bit pointer is kept (and spilled) in VGPRs -- a spill
+      // reload costs an s_waitcnt vmcnt(0), which would also wait for this
+      // prefetch.  Issued unconditionally (straight-line vmcnt accounting, as
+      // the PCM stores): past the chunk the resources have no records.
+      const bool more = g + 1 < end;
+      uint4 pd = {0, 0, 0, 0};
+      {
+        load_lines(coef, g + 1, lane, cw, more ? (int)(MP3G_COEF_PER_GRANULE * sizeof(int16_t)) : 0);
+        if (lane < 10) {
+          const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+              const_cast<mp3g_granule*>(gran + g + 1), (short)0, more ? (int)sizeof(mp3g_granule) : 0, 0x00020000);
+          const auto v = __builtin_amdgcn_raw_buffer_load_b128(rd, lane * 16, 0, 0);
+          pd = make_uint4(v[0], v[1], v[2], v[3]);
         }
       }
-    }
-    const int count1 = (int)(d0 & 0xffffu);
-    const bool shortblk = is_short(d1);
-    const bool mixed = (d1 >> 24) != 0;
-    wave_sync();
-    stamp(0);
 
-    // ---- front end: requantize (gather through the reorder), lane = (ch, sb = k) ----
-    // the lane's 18 line-info words and raw integers are loaded in bulk first
-    float x[18];
-    if (all_long) {
-      int xi[18];
+      // ---- matrixing (frame.go:642-648): S rows into the ring (lane (ch, sb)
+      //      writes its 18 slots), then one lane per (ch, slot) turns its row into
+      //      the 32 distinct values X of V = synthNWin * S with an in-lane fast
+      //      DCT-II-32 on float pairs (dct32.h), in place ----
+      if (need_v && act) {
 #pragma unroll
-      for (int q = 0; q < 9; q++) {
-        xi[2 * q] = (int)(int16_t)(cw[q] & 0xffffu);
-        xi[2 * q + 1] = (int)(int16_t)(cw[q] >> 16);
-      }
-      // long band of line j: first band of the subband + band starts among
-      // lines 1..j.  Every long band starts at an even line (consts.go:68-97
-      // SfBandIndices; dsp_tables.cpp checks it), so lines 2q and 2q + 1
-      // share one band: one exponent read per line pair.
-      const uint32_t lb = sh.lband[combo][k];
-      _Float16 ex[9];
-#pragma unroll
-      for (int q = 0; q < 9; q++)
-        ex[q] = s.expo[22 * ch + (int)(lb & 31u) + __builtin_popcount((lb >> 5) & ((2u << (2 * q)) - 1u))];
-      // Lines >= count1 hold zeros (the bitstream parse's guarantee,
-      // maindata/huffman.go:130-134; mp3g_validate checks it), and requantizing
-      // 0 gives 0, so long blocks need no per-line count1 test here.
-      // (absent-channel lanes compute garbage that nothing reads)
-#pragma unroll
-      for (int j = 0; j < 18; j++) x[j] = requant_fast(xi[j], ex[j >> 1]);
-    } else {
-      int nsfs = 0;  // short bands whose first line lies below count1 (frame.go:229-255 loop bound)
-#pragma unroll
-      for (int b = 0; b < 13; b++) nsfs += 3 * (int)g_fast.sfb_short[combo][b] < count1;
-      // reorder gather: the channel's raw lines staged in the current slots of
-      // the ring, lane (ch, sb) writing its 9 dwords to column sb
-      {
-        uint32_t* col = reinterpret_cast<uint32_t*>(&s.ring[ch][k][kHist]);
-#pragma unroll
-        for (int q = 0; q < 9; q++) col[q] = cw[q];
+        for (int j = 0; j < 18; j++) s.ring[ch][k][kHist + j] = o[j];
       }
       wave_sync();
-      const int16_t* rch = reinterpret_cast<const int16_t*>(&s.ring[ch][0][kHist]);
-      // line info through a buffer resource (SGPR base, 32-bit lane offset) and
-      // the lane's first line recomputed here: nothing of this rare path stays
-      // live (in VGPRs) across the granule loop
-      const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
-          const_cast<uint32_t*>(&g_fast.linfo[combo][0]), (short)0, 576 * 4, 0x00020000);
-      const int L0 = 18 * (lane_fresh() & 31);
-#pragma unroll
-      for (int j = 0; j < 18; j++) {
-        const int L = L0 + j;
-        const uint32_t inf = __builtin_amdgcn_raw_buffer_load_b32(rl, 4 * L, 0, 0);
-        const int sfl = inf & 31, sfs = (inf >> 5) & 15, wsrc = (inf >> 9) & 3, wown = (inf >> 11) & 3;
-        const int srcr = inf >> 13;
-        const bool longlike = !shortblk || (mixed && L < 36);
-        const bool started = sfs < nsfs;
-        const bool reord = sfs == (mixed ? 3 : 0) || started;
-        const int src = seli(longlike || !reord, L, srcr);
-        const int win = seli(reord, wsrc, wown);
-        const int eidx = seli(longlike, 22 * ch + sfl, 44 + 39 * ch + 3 * sfs + win);
-        const bool process = longlike ? (shortblk || L < count1) : started;
-        const int sk = (src * 3641) >> 16;  // src / 18 for src < 576
-        const int xi = rch[2 * kSlots * sk + (src - 18 * sk)];
-        x[j] = self(process, requant_fast(xi, s.expo[eidx]), (float)xi);
-      }
-      wave_sync();  // staged lines read before the slots are reused
-    }
-    stamp(1);
-    // ---- MS / intensity stereo with the partner channel's lane (frame.go:304-420) ----
-    if (nch == 2 && hdr_mode(h) == 1 && (h & 0x30u)) {
-      const mp3g_channel& C0 = s.desc.ch[0];
-      const int c1r = (int)(cp0[1] & 0xffffu);
-      const int msmax = max((int)(cp0[0] & 0xffffu), c1r);
-#ifdef MP3G_EXP_NOIS
-      const bool ms = h & 0x20u, is = false;  // timing experiment only: wrong PCM
-#else
-      const bool ms = h & 0x20u, is = h & 0x10u;
-#endif
-      const bool short0 = is_short(cp1[0]);
-      const bool mixed0 = (cp1[0] >> 24) != 0;
-      const float inv_sqrt2 = 0.70710678118654752440f;
-      if (ms) {
-        // MS: L' = (l + r)c, R' = (l - r)c for lines below max(count1)
-        // (frame.go:362-377).  Two lines per step: one swap gives lanes < 32
-        // (l, r) of line j and lanes >= 32 those of line j + 1, (l + r)c,
-        // (l - r)c in one packed pair, a second swap hands back L' / R' of
-        // both lines to their channels' lanes.  Long blocks without intensity
-        // stereo transform every line: at or above max(count1) both channels
-        // are 0, where (l +- r)c is 0 too.  Otherwise lines >= max(count1) keep
-        // their values (the reorder can move values past count1; IS follows).
-        auto ms_pair = [&](float& u, float& v) {
-          const auto r = __builtin_amdgcn_permlane32_swap(__float_as_int(u), __float_as_int(v), false, false);
-          const float a = __int_as_float(r[0]), b = __int_as_float(r[1]);
-          const f2 pq = (f2){a + b, a - b} * bcast(inv_sqrt2);
-          const auto r2 = __builtin_amdgcn_permlane32_swap(__float_as_int(pq.x), __float_as_int(pq.y), false, false);
-          u = __int_as_float(r2[0]);
-          v = __int_as_float(r2[1]);
-        };
-        if (all_long && !is) {  // wave-uniform
-#pragma unroll
-          for (int j = 0; j < 18; j += 2) ms_pair(x[j], x[j + 1]);
-        } else {
-          const int left = msmax - 18 * (lane_fresh() & 31);  // lines of this subband below msmax
-#pragma unroll
-          for (int j = 0; j < 18; j += 2) {
-            float n0 = x[j], n1 = x[j + 1];
-            ms_pair(n0, n1);
-            x[j] = j < left ? n0 : x[j];
-            x[j + 1] = j + 1 < left ? n1 : x[j + 1];
-          }
-        }
-      }
-      if (is) {
-        // Intensity stereo per line of this lane (frame.go:308-359, :379-419):
-        // bands at or above channel 1's count1, ratio index from CHANNEL 0's
-        // scale factors, each channel scaled by its own ratio (is_pos 7 = no
-        // change: isr[7] = (1, 1)).  Long blocks: the line's band from the
-        // subband's band-start mask (as in the requantization); short / mixed
-        // blocks: the line info table.
-        const int k0 = lane_fresh() & 31;
-        int nl_is = 0, ns_is = 0;  // first long / short band starting at or above channel 1's count1
-#pragma unroll
-        for (int b = 0; b < 23; b++) nl_is += (int)g_fast.sfb_long[combo][b] < c1r;
-#pragma unroll
-        for (int b = 0; b < 14; b++) ns_is += 3 * (int)g_fast.sfb_short[combo][b] < c1r;
-        if (!short0) {
-          const uint32_t lb = sh.lband[combo][k0];
-#pragma unroll
-          for (int j = 0; j < 18; j++) {
-            const int sfl = (int)(lb & 31u) + __builtin_popcount((lb >> 5) & ((2u << j) - 1u));
-            const int pos = min((int)C0.scalefac_l[min(sfl, 21)], 7);
-            const float rr = sh.isr[pos][ch];
-            x[j] = (sfl < 21 && sfl >= nl_is) ? x[j] * rr : x[j];
-          }
-        } else {
-          const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
-              const_cast<uint32_t*>(&g_fast.linfo[combo][0]), (short)0, 576 * 4, 0x00020000);
-#pragma unroll
-          for (int j = 0; j < 18; j++) {
-            const uint32_t info = __builtin_amdgcn_raw_buffer_load_b32(rl, 4 * (18 * k0 + j), 0, 0);
-            const int sfl = info & 31, sfs = (info >> 5) & 15, wown = (info >> 11) & 3;
-            const bool lp = mixed0 && sfl < 8 && sfl >= nl_is;
-            const bool sp = sfs < 12 && (!mixed0 || sfs >= 3) && sfs >= ns_is;
-            const int pl = lp ? min((int)C0.scalefac_l[min(sfl, 21)], 7) : 7;
-            const int ps = sp ? min((int)C0.scalefac_s[min(sfs, 12)][min(wown, 2)], 7) : 7;
-            x[j] = x[j] * sh.isr[pl][ch] * sh.isr[ps][ch];
-          }
-        }
-      }
-    }
-    {
-      const bool sw = shortblk;
-      const bool skip = !act || (sw && !mixed);
-      const int sblim = (sw && mixed) ? 2 : 32;
-      const bool lower = !skip && k >= 1 && k < sblim;     // butterfly with subband k-1
-      const bool upper = !skip && k < 31 && k + 1 < sblim;  // butterfly with subband k+1
-      float up[8], dn[8];
-#pragma unroll
-      for (int i = 0; i < 8; i++) {
-        up[i] = xl::from_prev(x[17 - i]);  // x_{k-1}[17-i]
-        dn[i] = xl::from_next(x[i]);       // x_{k+1}[i]
-      }
-#pragma unroll
-      for (int i = 0; i < 8; i++) {
-        const float cs = g_fast.aa_cs[i], ca = g_fast.aa_ca[i];
-        const float ui = x[i], li = x[17 - i];
-        x[i] = self(lower, ui * cs + up[i] * ca, ui);
-        x[17 - i] = self(upper, li * cs - dn[i] * ca, li);
-      }
-    }
-
-    stamp(2);
-    // ---- IMDCT + overlap + frequency inversion ----
-    float o[18];
-    {
-      // mixed blocks: long windows for subbands 0, 1 whenever win_switch && mixed (frame.go:462-466)
-      int bt = (int)((d1 >> 16) & 3u);
-      if ((d1 & 0xff00ff00u) == 0x01000100u && k < 2) bt = 0;
-      // raw[0..17] + old overlap -> o[], raw[18..35] -> new overlap, written as
-      // each raw value is produced (no 36-entry temporary); frequency
-      // inversion rides on the signs of the windows and of stp
-      if (bt == 2) {
-        float st[18];
-#pragma unroll
-        for (int q = 0; q < 9; q++) {
-          st[q] = stp[q].x;
-          st[17 - q] = stp[q].y;
-        }
-        // raw[pos] = sum over the windows wi with 0 <= pos-6-6wi < 12 of
-        // (sum_m x[wi+3m] cosN12[m][p]) * win[2][p], p = pos-6-6wi (imdct.go:88-94)
-#pragma unroll
-        for (int pos = 0; pos < 36; pos++) {
-          float raw = 0.0f;
-#pragma unroll
-          for (int wi = 0; wi < 3; wi++) {
-            const int p = pos - 6 - 6 * wi;
-            if (p < 0 || p >= 12) continue;
-            float sum = 0.0f;
-#pragma unroll
-            for (int m = 0; m < 6; m++) sum += x[wi + 3 * m] * dct4::kCos12[p][m];
-            raw += sum * dct4::kWin12[p];
-          }
-          if (pos & 1) raw *= sodd;  // (pos and pos - 18 have the same parity)
-          if (pos < 18) o[pos] = raw + st[pos];
-          else st[pos - 18] = self(act, raw, st[pos - 18]);
-        }
-#pragma unroll
-        for (int q = 0; q < 9; q++) stp[q] = (f2){st[q], st[17 - q]};
-      } else {
-        // the 18 distinct sums are a DCT-IV of size 18 (dct4_18.h):
-        // sum_m x[m] cosN36[m][q] = X[9+q], sum_m x[m] cosN36[m][18+q] = -X[8-q];
-        // packed, pair k = (X[2k], X[17-2k]) holds X[9+q] and X[8-q] of one q
-        f2 P[9];
-        dct4::dct4_18_pk(x, P);
-        const float4* Wq = sh.winp[bt][lane_fresh() & 1];
-        // (the overlap of an absent channel stays frozen: frame.go Decode
-        // touches ch < nch only; stereo granules need no per-lane select)
-        auto overlap = [&](auto frozen) {
-#pragma unroll
-          for (int kk = 0; kk < 9; kk++) {
-            const int q = kk <= 4 ? 8 - 2 * kk : 2 * kk - 9;
-            const float za = kk <= 4 ? P[kk].y : P[kk].x;  // X[9+q]
-            const float zb = kk <= 4 ? P[kk].x : P[kk].y;  // X[8-q]
-            const float4 w = Wq[q];
-            // (o[q], o[17-q]) = X[9+q] (W[q], -W[17-q]) + stp[q];
-            // new stp[q] = X[8-q] (-W[18+q], -W[35-q])   (signs folded in w)
-            const f2 oq = pfma(bcast(za), (f2){w.x, w.y}, stp[q]);
-            o[q] = oq.x;
-            o[17 - q] = oq.y;
-            const f2 ns = bcast(zb) * (f2){w.z, w.w};
-            if constexpr (decltype(frozen)::value)
-              stp[q] = (f2){self(act, ns.x, stp[q].x), self(act, ns.y, stp[q].y)};
-            else
-              stp[q] = ns;
-          }
-        };
-        if (nch == 2) overlap(std::false_type{});
-        else overlap(std::true_type{});
-      }
-    }
-    stamp(3);
-    // prefetch the next granule: lands during the matrixing and window phases
-    // (issued here, not at the top, so its 13 VGPRs are not live across the
-    // front end and IMDCT); buffer resources with SGPR bases and 32-bit lane
-    // offsets: no 64-bit pointer is kept (and spilled) in VGPRs -- a spill
-    // reload costs an s_waitcnt vmcnt(0), which would also wait for this
-    // prefetch
-    const bool more = g + 1 < end;
-    uint4 pd = {0, 0, 0, 0};
-#if MP3G_FAST_STRAIGHT
-    // issued unconditionally (straight-line vmcnt accounting, as the PCM
-    // stores below): past the chunk the resources have no records
-    {
-      load_lines(coef, g + 1, lane, cw, more ? (int)(MP3G_COEF_PER_GRANULE * sizeof(int16_t)) : 0);
-      if (lane < 10) {
-        const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<mp3g_granule*>(gran + g + 1), (short)0, more ? (int)sizeof(mp3g_granule) : 0, 0x00020000);
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rd, lane * 16, 0, 0);
-        pd = make_uint4(v[0], v[1], v[2], v[3]);
-      }
-    }
-#else
-    if (more) {
-      load_lines(coef, g + 1, lane, cw);
-      if (lane < 10) {
-        const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<mp3g_granule*>(gran + g + 1), (short)0, (int)sizeof(mp3g_granule), 0x00020000);
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rd, lane * 16, 0, 0);
-        pd = make_uint4(v[0], v[1], v[2], v[3]);
-      }
-    }
-#endif
-
-    // ---- matrixing (frame.go:642-648): S rows into the ring (lane (ch, sb)
-    //      writes its 18 slots), then one lane per (ch, slot) turns its row into
-    //      the 32 distinct values X of V = synthNWin * S with an in-lane fast
-    //      DCT-II-32 on float pairs (dct32.h), in place ----
-    if (need_v && act) {
-#pragma unroll
-      for (int j = 0; j < 18; j++) s.ring[ch][k][kHist + j] = o[j];
-    }
-    wave_sync();
-    stamp(4);
-    {
-      const int slot = lane & 31;  // lane = (ch, slot), slots 0..17
-      if (need_v && act && slot < 18) {
-        float* colu = &s.ring[ch][0][kHist + slot];  // S[k] / X at colu[kSlots * k]
-        dct32::f2 sp[16];
-#pragma unroll
-        for (int q = 0; q < 16; q++) sp[q] = (dct32::f2){colu[kSlots * 2 * q], colu[kSlots * (2 * q + 1)]};
-#ifdef MP3G_EXP_NODCT
-        // timing experiment only: X = S (wrong PCM)
-#pragma unroll
-        for (int t = 0; t < 16; t++) {
-          colu[kSlots * dct32::kColX[t]] = sp[t].x;
-          colu[kSlots * dct32::kColY[t]] = sp[t].y;
-        }
-        if (false)
-#endif
-        dct32::dct2_32_to(sp, [&](int t, dct32::f2 v) {
-          colu[kSlots * dct32::kColX[t]] = v.x;
-          colu[kSlots * dct32::kColY[t]] = v.y;
-        });
-      }
-    }
-    stamp(5);
-    wave_sync();  // ring slots of this granule written before the window reads them
-
-    // ---- next granule in: raw/eo (dead after the matrixing) and the
-    //      descriptor (not read again this granule) take the prefetch now,
-    //      before the PCM stores are issued -- vmcnt counts loads and stores in
-    //      issue order, so a wait for the prefetch after the stores would wait
-    //      for the stores too ----
-    if (more && lane < 10) reinterpret_cast<uint4*>(&s.desc)[lane] = pd;
-
-    // ---- 16-tap window over the X ring -> s16 PCM, stored straight to HBM ----
-    // (lanes of an absent channel compute values that are never stored)
-    if (out) {
-      float dw[16];
+      stamp(4);
       {
-        const float4* d4 = reinterpret_cast<const float4*>(&sh.dwin[k][0]);
+        const int slot = lane & 31;  // lane = (ch, slot), slots 0..17
+        if (need_v && act && slot < 18) {
+          float* colu = &s.ring[ch][0][kHist + slot];  // S[k] / X at colu[kSlots * k]
+          dct32::f2 sp[16];
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-          const float4 v = d4[q];
-          dw[4 * q] = v.x;
-          dw[4 * q + 1] = v.y;
-          dw[4 * q + 2] = v.z;
-          dw[4 * q + 3] = v.w;
+          for (int q = 0; q < 16; q++) sp[q] = (dct32::f2){colu[kSlots * 2 * q], colu[kSlots * (2 * q + 1)]};
+          dct32::dct2_32_to(sp, [&](int t, dct32::f2 v) {
+            colu[kSlots * dct32::kColX[t]] = v.x;
+            colu[kSlots * dct32::kColY[t]] = v.y;
+          });
         }
       }
-      // accumulator pair p = output slots (2p, 2p+1).  Tap 2t of the pair reads
-      // column a of rows (v, v+1) and tap 2t+1 column b of rows (v-1, v),
-      // v = 2p - 2t: every operand pair is two rows of one column, i.e. one
-      // ds_read2_b32 that lands as the packed operand, and each feeds up to 8
-      // accumulator pairs.
-      const f2* RA = reinterpret_cast<const f2*>(&s.ring[ch][pa][0]);
-      const float* RB = &s.ring[ch][pb][0];
-      f2 acc2[9];
+      stamp(5);
+      wave_sync();  // ring slots of this granule written before the window reads them
+
+      // ---- next granule in: the descriptor (not read again this granule)
+      //      takes the prefetch now, before the PCM stores are issued -- vmcnt
+      //      counts loads and stores in issue order, so a wait for the
+      //      prefetch after the stores would wait for the stores too ----
+      if (more && lane < 10) reinterpret_cast<uint4*>(&s.desc)[lane] = pd;
+
+      // ---- 16-tap window over the X ring -> s16 PCM, stored straight to HBM ----
+      // (lanes of an absent channel compute values that are never stored)
+      if (out) {
+        float dw[16];
+        {
+          const float4* d4 = reinterpret_cast<const float4*>(&sh.dwin[k][0]);
 #pragma unroll
-      for (int p = 0; p < 9; p++) acc2[p] = bcast(0.0f);
-#pragma unroll
-      for (int v = -14; v <= 16; v += 2) {
-        const f2 A = RA[(kHist + v) / 2];  // slots (16+v, 17+v): 8-B aligned
-        const f2 B = {RB[kHist + v - 1], RB[kHist + v]};
-#pragma unroll
-        for (int t = 0; t < 8; t++) {
-          const int p = v / 2 + t;
-#ifdef MP3G_EXP_HALFWIN
-          if (t & 1) continue;  // timing experiment only: half the taps (wrong PCM)
-#endif
-          if (p >= 0 && p < 9) {
-            acc2[p] = pfma(bcast(dw[2 * t]), A, acc2[p]);
-            acc2[p] = pfma(bcast(dw[2 * t + 1]), B, acc2[p]);
+          for (int q = 0; q < 4; q++) {
+            const float4 v = d4[q];
+            dw[4 * q] = v.x;
+            dw[4 * q + 1] = v.y;
+            dw[4 * q + 2] = v.z;
+            dw[4 * q + 3] = v.w;
           }
         }
-      }
-      // (L, R) sample pairs without LDS staging: one v_permlane32_swap per slot
-      // pair hands lane i slot 2p's (L, R) and lane 32 + i slot 2p + 1's, so
-      // every lane stores one dword per slot pair and the wave 2 x 128
-      // contiguous bytes.  Mono: the swap hands lane i channel 0's slot 2p and
-      // lane 32 + i its slot 2p + 1, stored in both halves (frame.go:671-678).
-      auto pack = [&](auto mono) {
+        // accumulator pair p = output slots (2p, 2p+1).  Tap 2t of the pair reads
+        // column a of rows (v, v+1) and tap 2t+1 column b of rows (v-1, v),
+        // v = 2p - 2t: every operand pair is two rows of one column, i.e. one
+        // ds_read2_b32 that lands as the packed operand, and each feeds up to 8
+        // accumulator pairs.
+        const f2* RA = reinterpret_cast<const f2*>(&s.ring[ch][pa][0]);
+        const float* RB = &s.ring[ch][pb][0];
+        f2 acc2[9];
 #pragma unroll
-        for (int p = 0; p < 9; p++) {
-          const int a = (int)__builtin_amdgcn_fmed3f(acc2[p].x, -32767.0f, 32767.0f);
-          const int b = (int)__builtin_amdgcn_fmed3f(acc2[p].y, -32767.0f, 32767.0f);
-          const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
-          // low halves of (r[0], r[1]) -> one dword: L | R << 16 (R = L for mono)
-          pk[p] = __builtin_amdgcn_perm((uint32_t)(decltype(mono)::value ? r[0] : r[1]), (uint32_t)r[0], 0x05040100u);
+        for (int p = 0; p < 9; p++) acc2[p] = bcast(0.0f);
+#pragma unroll
+        for (int v = -14; v <= 16; v += 2) {
+          const f2 A = RA[(kHist + v) / 2];  // slots (16+v, 17+v): 8-B aligned
+          const f2 B = {RB[kHist + v - 1], RB[kHist + v]};
+#pragma unroll
+          for (int t = 0; t < 8; t++) {
+            const int p = v / 2 + t;
+            if (p >= 0 && p < 9) {
+              acc2[p] = pfma(bcast(dw[2 * t]), A, acc2[p]);
+              acc2[p] = pfma(bcast(dw[2 * t + 1]), B, acc2[p]);
+            }
+          }
         }
-      };
-      if (nch == 2) pack(std::false_type{});
-      else pack(std::true_type{});
-      // stored right away: a store's data registers are free again once it
-      // has issued (no s_waitcnt before their reuse on gfx950), and the loads
-      // this wave waits for next were issued before these stores
-#if !MP3G_FAST_STRAIGHT
-      uint32_t* P = reinterpret_cast<uint32_t*>(pcm + (size_t)g * 1152);
-#pragma unroll
-      for (int p = 0; p < 9; p++) {
-#if MP3G_FAST_NT_STORE
-        __builtin_nontemporal_store(pk[p], &P[32 * (2 * p + hi) + k]);
-#else
-        P[32 * (2 * p + hi) + k] = pk[p];
-#endif
+        // stored right away: a store's data registers are free again once it
+        // has issued (no s_waitcnt before their reuse on gfx950), and the loads
+        // this wave waits for next were issued before these stores
+        pack_pcm(acc2, P.nch, pk);
       }
-#endif
-    }
-#if MP3G_FAST_STRAIGHT
-    {
-      // issued for replayed granules too, through a resource with no records
-      const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
-          pcm + (size_t)g * 1152, (short)0, out ? MP3G_PCM_BYTES_PER_GRANULE : 0, 0x00020000);
-#pragma unroll
-      for (int p = 0; p < 9; p++)
-        __builtin_amdgcn_raw_buffer_store_b32(pk[p], rp, 4 * (32 * (2 * p + hi) + k), 0, MP3G_FAST_NT_STORE ? 2 : 0);
-    }
-#endif
-#ifndef MP3G_EXP_NOSYNC_SHIFT
-    wave_sync();  // ring reads done
-#endif
-    stamp(6);
+      store_pcm(pcm, g, out, pk, hi, k);
+      wave_sync();  // ring reads done
+      stamp(6);
 
-    // ---- history shift (channels this granule touched): lane = (c, column),
-    //      slots 18..33 -> 0..15 as 8-B moves; not after a replayed granule
-    //      whose V feeds nothing (its slots hold no X; the next granule is a
-    //      replay too and rewrites the history before any window reads it) ----
-    if (ch < nch && need_v) {
-      f2* col = reinterpret_cast<f2*>(&s.ring[ch][k][0]);
+      // ---- history shift (channels this granule touched): lane = (c, column),
+      //      slots 18..33 -> 0..15 as 8-B moves; not after a replayed granule
+      //      whose V feeds nothing (its slots hold no X; the next granule is a
+      //      replay too and rewrites the history before any window reads it) ----
+      if (ch < P.nch && need_v) {
+        f2* col = reinterpret_cast<f2*>(&s.ring[ch][k][0]);
 #pragma unroll
-      for (int q = 0; q < 8; q++) col[q] = col[9 + q];
+        for (int q = 0; q < 8; q++) col[q] = col[9 + q];
+      }
+      wave_sync();
+      stamp(7);
     }
-#ifndef MP3G_EXP_NOSYNC_SHIFT2
-    wave_sync();
-#endif
-    stamp(7);
   }
   if constexpr (kStamp) rt[2] = __builtin_amdgcn_s_memrealtime();
 
-  if (cd.flags & kChunkStateOut) {
+  // Frame.store / vVec after the chunk's last granule (frame.go:48-49)
+  auto export_state = [&](const f2 (&st)[9]) {
+    if (!(cd.flags & kChunkStateOut)) return;
     mp3g_state* so = state_out + cd.stream;
+    const int c = lane_fresh() >> 5, kk = lane_fresh() & 31;
+    const float sg = (kk & 1) ? -1.0f : 1.0f;
 #pragma unroll
     for (int q = 0; q < 9; q++) {
-      so->store[ch][k][q] = (q & 1) ? stp[q].x * sodd : stp[q].x;
-      so->store[ch][k][17 - q] = (q & 1) ? stp[q].y : stp[q].y * sodd;
+      so->store[c][kk][q] = (q & 1) ? st[q].x * sg : st[q].x;
+      so->store[c][kk][17 - q] = (q & 1) ? st[q].y : st[q].y * sg;
     }
     for (int e = lane; e < 2 * 1024; e += kLanes) {
       const int c = e >> 10, blk = (e >> 6) & 15, i = e & 63;
       so->vvec[c][64 * blk + i] = blk < 15 ? v_from_x(&s.ring[c][0][kHist - 1 - blk], i) : 0.0f;
     }
+  };
+  export_state(stp);
+
+  // ---- hot zones (rare): redo their granules in the reference's order from
+  //      their replay start (exact entry state) and overwrite their PCM; a
+  //      zone ends two granules after the last hot granule it meets.  Past
+  //      a zone the fast pass's own output stands: it depends on no hot
+  //      granule's hybrid output.  A zone reaching the chunk end also rewrites
+  //      the exported state. ----
+  if (nz) {
+    f2 zst[9];  // the zones' own overlap state (nothing flows in from the fast pass)
+    uint32_t done = 0;  // the exact state in zst / the ring is valid for granules < done
+    bool have = false;
+    for (uint32_t i = 0; i < nz; i++) {
+      const uint32_t zs = __builtin_amdgcn_readfirstlane(s.zone[i][0]);
+      uint32_t ze = __builtin_amdgcn_readfirstlane(s.zone[i][1]);
+      if (have && ze <= done) continue;
+      uint32_t g = done;
+      if (!have || zs > done) {  // a fresh zone: replay from its start's replay start
+        ChunkDesc cr = cd;
+        cr.out_first = zs;
+        cr.n_out = end - zs;
+        uint64_t wz;
+        int zin[2];
+        prologue(cr, gran, &wz, zin, lane);
+        init_state(s, sin, zin, lane_fresh(), zst);
+        g = __builtin_amdgcn_readfirstlane((uint32_t)wz);
+        have = true;
+      }
+      for (; g < ze; g++) {
+        const bool need_v = replay_needs_v(gran, g, zs, s);
+        if (exact_granule(gran, coef, pcm, s, sh, g, g >= zs, need_v, zst)) ze = g + 2 > ze ? (g + 2 < end ? g + 2 : end) : ze;
+      }
+      done = g;
+    }
+    if (done >= end) export_state(zst);
   }
   if constexpr (kStamp) {
     rt[3] = __builtin_amdgcn_s_memrealtime();

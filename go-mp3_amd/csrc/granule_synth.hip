@@ -11,11 +11,11 @@
 // north star's "polyphase kernel at >= 40 % of the HBM roof" is priced on
 // (SURVEY.md 8(d)).
 //
-// Work decomposition: the fused kernel's plans, one wave per chunk.  The
-// window of slot ss reads the 15 preceding V blocks, so a chunk replays only
-// the granule before it (matrixing, no window) when that granule has both
-// channels; otherwise it takes the fused kernel's replay start (a superset).
-// Per granule:
+// Work decomposition: the fused kernel's plans, one wave per chunk, eight
+// chunks per workgroup.  The window of slot ss reads the 15 preceding V
+// blocks, so a chunk replays only the granule before it (matrixing, no
+// window) when that granule has both channels; otherwise it takes the fused
+// kernel's replay start (a superset).  Per granule:
 //   load      the granule's nch x 576 floats as 8-B pairs, lane + 64 r
 //             (coalesced, one granule ahead in registers); the resource is
 //             sized to nch x 2,304 B, so a mono granule reads nothing of [1];
@@ -24,41 +24,126 @@
 //   matrixing lane (ch, slot < 18): S column -> 32 X values in place;
 //   window    lane (ch, i): 16 taps, 18 outputs, s16 (L, R) pairs stored;
 //   shift     slots 18..33 -> 0..15.
+// Hot granules (a line above kHotS) and the granule after each are redone in
+// the reference's order after the chunk's fast pass (as in the fused kernel).
 // (compiled in kernels_fast.hip after granule_fast.hip: shares its helpers)
 
 namespace mp3g {
 namespace v3 {
 
-#ifndef MP3G_SYNTH_WG_WAVES
-#define MP3G_SYNTH_WG_WAVES 8
-#endif
-constexpr int kSynthWaves = MP3G_SYNTH_WG_WAVES;
-// granules of lines in flight per wave (register buffers of 18 VGPRs)
-#ifndef MP3G_SYNTH_DEPTH
-#define MP3G_SYNTH_DEPTH 1  // 2 measured the same at c3 and 2 % slower at c2
-#endif
-#ifndef MP3G_SYNTH_DW_REGS
-#define MP3G_SYNTH_DW_REGS 1
-#endif
-#ifndef MP3G_SYNTH_PRIO
-#define MP3G_SYNTH_PRIO 1  // c2 -3.5 %, c3 +-0 (tools/gpu_synthab.sh)
-#endif
-// cache-policy bits of the line loads / PCM stores (experiments)
-#ifndef MP3G_SYNTH_LOAD_AUX
-#define MP3G_SYNTH_LOAD_AUX 0
-#endif
-#ifndef MP3G_SYNTH_STORE_AUX
-#define MP3G_SYNTH_STORE_AUX 2  // non-temporal PCM stores: c3 -1.3 %, c2 -2 % (the lines: nt loads +5 %)
-#endif
+constexpr int kSynthWaves = 8;
 
 struct __align__(16) SynthWaveSmem {
   float ring[2][32][kSlots];
+  uint32_t zone[kZones][2];  // hot zones of the chunk (record_hot)
 };
 
-#ifndef MP3G_SYNTH_WAVES_PER_SIMD
-#define MP3G_SYNTH_WAVES_PER_SIMD 4
-#endif
-__global__ void __launch_bounds__(kLanes * kSynthWaves, MP3G_SYNTH_WAVES_PER_SIMD)
+namespace {
+
+// The granule's lines as 8-B pairs: pair p = lane + 64 r of [nch][576].
+// Issued unconditionally (straight-line vmcnt accounting): past the chunk
+// (or with nbytes 0) the resource has no records, so the loads return 0 and
+// touch no memory.
+__device__ __forceinline__ void synth_load(const float* lines, uint32_t g, uint32_t nbytes, int lane, f2 v[9]) {
+  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(lines + (size_t)g * MP3G_COEF_PER_GRANULE), (short)0, (int)nbytes, 0x00020000);
+#pragma unroll
+  for (int r = 0; r < 9; r++) {
+    const auto u = __builtin_amdgcn_raw_buffer_load_b64(rc, 8 * lane + 512 * r, 0, 0);
+    v[r] = (f2){__uint_as_float(u[0]), __uint_as_float(u[1])};
+  }
+}
+
+// stage: line 18 sb + ss of channel c -> ring[c][sb][16 + ss], as 8-B pairs
+// (ds_write_b64, 4 x 16 lanes: as separate dwords the 32 lanes of a write
+// group land on 16 even banks)
+__device__ __forceinline__ void synth_stage(SynthWaveSmem& s, const f2 buf[9], int nch) {
+#pragma unroll
+  for (int r = 0; r < 9; r++) {
+    const int e = 2 * lane_fresh() + 128 * r;  // first line of the pair in [2][576]
+    const int c = e >= 576;
+    const int l = e - 576 * c;
+    const int sb = (l * 3641) >> 16;  // l / 18 for l < 576
+    f2* colp = reinterpret_cast<f2*>(&s.ring[c][0][0]);
+    if (c < nch) colp[17 * sb + kHist / 2 + ((l - 18 * sb) >> 1)] = buf[r];
+  }
+}
+
+__device__ __forceinline__ float max_abs_pairs(const f2 v[9]) {
+  float m = 0.0f;
+#pragma unroll
+  for (int r = 0; r < 9; r++) m = fmaxf(m, fmaxf(fabsf(v[r].x), fabsf(v[r].y)));
+  return m;
+}
+
+// Replay start of a synthesis chunk beginning at c0: the granule before it
+// when that granule carries both channels' history, else the fused kernel's
+// decision (a superset).
+__device__ __forceinline__ uint32_t synth_replay_start(const ChunkDesc& cd, uint64_t c0, const mp3g_granule* gran,
+                                                       int init_in[2], int lane) {
+  const uint64_t s0 = cd.stream_first;
+  const bool have_in = cd.flags & kChunkStateIn;
+  uint64_t w64;
+  if (c0 > s0 && hdr_nch(gran[c0 - 1].header) == 2) {
+    w64 = c0 - 1;
+    init_in[0] = init_in[1] = (w64 == s0) && have_in;
+  } else {
+    ChunkDesc cr = cd;
+    cr.n_out = (uint32_t)(cd.out_first + cd.n_out - c0);
+    cr.out_first = c0;
+    prologue(cr, gran, &w64, init_in, lane);
+  }
+  return __builtin_amdgcn_readfirstlane((uint32_t)w64);
+}
+
+// V history of a replay start: X vectors from the stream's state_in or zero.
+__device__ __forceinline__ void synth_init_ring(SynthWaveSmem& s, const mp3g_state* sin, const int init_in[2],
+                                                int lane) {
+  const bool in0 = init_in[0] && sin, in1 = init_in[1] && sin;
+  for (int e = lane; e < 2 * 15 * 32; e += kLanes) {
+    const int c = e / (15 * 32), blk = (e >> 5) % 15, m = e & 31;
+    const bool in = c ? in1 : in0;
+    s.ring[c][dct32::kPosOfM[m]][kHist - 1 - blk] = in ? x_from_v(&sin->vvec[c][64 * blk], m) : 0.0f;
+  }
+}
+
+// One granule in the reference's operation order (hot-zone fixup); returns
+// whether it is hot.
+__device__ __forceinline__ bool synth_exact_granule(const mp3g_granule* __restrict__ gran,
+                                                    const float* __restrict__ lines, int16_t* __restrict__ pcm,
+                                                    SynthWaveSmem& s, uint32_t g, bool out) {
+  const int lane = lane_fresh();
+  const int ch = lane >> 5, k = lane & 31, hi = lane >> 5;
+  const int nch = hdr_nch(__builtin_amdgcn_readfirstlane(gran[g].header));
+  f2 buf[9];
+  synth_load(lines, g, nch * 2304u, lane, buf);
+  const bool hot = __builtin_amdgcn_ballot_w64(max_abs_pairs(buf) > kHotS) != 0;
+  synth_stage(s, buf, nch);
+  wave_sync();
+  if (ch < nch && (lane & 31) < 18) matrix_exact(&s.ring[ch][0][kHist + (lane & 31)]);
+  wave_sync();
+  uint32_t pk[9] = {};
+  if (out) {
+    const int pa = dct32::kPosOfM[k < 16 ? 16 + k : (k == 16 ? 0 : 48 - k)];
+    const int pb = dct32::kPosOfM[k < 16 ? 16 - k : k - 16];
+    f2 acc2[9];
+    window_exact(&s.ring[ch][pa][0], &s.ring[ch][pb][0], k, acc2);
+    pack_pcm(acc2, nch, pk);
+  }
+  store_pcm(pcm, g, out, pk, hi, k);
+  wave_sync();
+  if (ch < nch) {
+    f2* col = reinterpret_cast<f2*>(&s.ring[ch][k][0]);
+#pragma unroll
+    for (int q = 0; q < 8; q++) col[q] = col[9 + q];
+  }
+  wave_sync();
+  return hot;
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(kLanes * kSynthWaves, 4)
 granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, const mp3g_granule* __restrict__ gran,
                      const float* __restrict__ lines, const mp3g_state* __restrict__ state_in,
                      mp3g_state* __restrict__ state_out, int16_t* __restrict__ pcm) {
@@ -76,53 +161,23 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
   const int pa = dct32::kPosOfM[k < 16 ? 16 + k : (k == 16 ? 0 : 48 - k)];
   const int pb = dct32::kPosOfM[k < 16 ? 16 - k : k - 16];
 
-  // replay start: the granule before the chunk when it carries both
-  // channels' history, else the fused kernel's decision (a superset)
-  uint64_t w64;
   int init_in[2];
-  {
-    const uint64_t c0 = cd.out_first, s0 = cd.stream_first;
-    const bool have_in = cd.flags & kChunkStateIn;
-    if (c0 > s0 && hdr_nch(gran[c0 - 1].header) == 2) {
-      w64 = c0 - 1;
-      init_in[0] = init_in[1] = (w64 == s0) && have_in;
-    } else {
-      prologue(cd, gran, &w64, init_in, lane);
-    }
-  }
-  const uint32_t w = __builtin_amdgcn_readfirstlane((uint32_t)w64);
+  const uint32_t w = synth_replay_start(cd, cd.out_first, gran, init_in, lane);
   const uint32_t out_first = __builtin_amdgcn_readfirstlane((uint32_t)cd.out_first);
   const uint32_t end = __builtin_amdgcn_readfirstlane((uint32_t)(cd.out_first + cd.n_out));
   const mp3g_state* sin = state_in ? state_in + cd.stream : nullptr;
-  {
-    const bool in0 = init_in[0] && sin, in1 = init_in[1] && sin;
-    for (int e = lane; e < 2 * 15 * 32; e += kLanes) {
-      const int c = e / (15 * 32), blk = (e >> 5) % 15, m = e & 31;
-      const bool in = c ? in1 : in0;
-      s.ring[c][dct32::kPosOfM[m]][kHist - 1 - blk] = in ? x_from_v(&sin->vvec[c][64 * blk], m) : 0.0f;
-    }
-  }
+  synth_init_ring(s, sin, init_in, lane);
 
-  // the granule's lines as 8-B pairs: pair p = lane + 64 r of [nch][576].
-  // Issued unconditionally (straight-line vmcnt accounting): past the chunk
-  // the resource has no records, so the loads return 0 and touch no memory.
   auto load = [&](uint32_t g, f2 v[9]) {
     const bool in = g < end;
     const uint32_t gg = in ? g : w;
     const uint32_t nch = in ? hdr_nch(__builtin_amdgcn_readfirstlane(gran[gg].header)) : 0u;
-    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(lines + (size_t)gg * MP3G_COEF_PER_GRANULE), (short)0, (int)(nch * 2304u), 0x00020000);
-#pragma unroll
-    for (int r = 0; r < 9; r++) {
-      const auto u = __builtin_amdgcn_raw_buffer_load_b64(rc, 8 * lane + 512 * r, 0, MP3G_SYNTH_LOAD_AUX);
-      v[r] = (f2){__uint_as_float(u[0]), __uint_as_float(u[1])};
-    }
+    synth_load(lines, gg, nch * 2304u, lane, v);
   };
   const int hi = lane >> 5;
   // the lane's 16 window taps, in registers for the whole chunk (read per
   // granule they were four 4-way bank-conflicted ds_read_b128)
   float dw[16];
-#if MP3G_SYNTH_DW_REGS
   {
     const float4* d4 = reinterpret_cast<const float4*>(&dwin_s[k][0]);
 #pragma unroll
@@ -134,27 +189,30 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
       dw[4 * q + 3] = v.w;
     }
   }
-#endif
 
-  // one granule; its lines in `buf`, which is refilled with granule g + depth
-  auto granule = [&](uint32_t g, f2 buf[9]) {
+  uint32_t nz = 0;  // hot zones recorded (s.zone)
+  uint32_t pk[9] = {};  // PCM of a granule (stale for replayed ones: stored to no records)
+  f2 A[9];
+  load(w, A);
+  wave_sync();
+  const uint32_t span = end - w, span2 = 2 * span, span3 = 3 * span;
+  for (uint32_t g = w; g < end; g++) {
+    // progress-balanced issue priority, as in the fused kernel (c2 -3.5 %)
+    const uint32_t left4 = 4u * (end - g);
+    if (left4 > span3) __builtin_amdgcn_s_setprio(3);
+    else if (left4 > span2) __builtin_amdgcn_s_setprio(2);
+    else if (left4 > span) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
     const uint32_t h = __builtin_amdgcn_readfirstlane(gran[g].header);
     const int nch = hdr_nch(h);
     const bool out = g >= out_first;
-    // ---- stage: line 18 sb + ss of channel c -> ring[c][sb][16 + ss] ----
-#pragma unroll
-    for (int r = 0; r < 9; r++) {
-      const int e = 2 * lane_fresh() + 128 * r;  // first line of the pair in [2][576]
-      const int c = e >= 576;
-      const int l = e - 576 * c;
-      const int sb = (l * 3641) >> 16;  // l / 18 for l < 576
-      // indexed as 8-B pairs (ds_write_b64, 4 x 16 lanes): as separate dwords
-      // the 32 lanes of a write group land on 16 even banks
-      f2* colp = reinterpret_cast<f2*>(&s.ring[c][0][0]);
-      if (c < nch) colp[17 * sb + kHist / 2 + ((l - 18 * sb) >> 1)] = buf[r];
-    }
-    // a later granule in flight during the matrixing and window
-    load(g + MP3G_SYNTH_DEPTH, buf);
+    // a hot granule: its zone is redone in the reference's order after the pass
+#if MP3G_HOT_CHECK
+    if (__builtin_amdgcn_ballot_w64(max_abs_pairs(A) > kHotS)) record_hot(s, nz, g, out_first, end);
+#endif
+    synth_stage(s, A, nch);
+    // the next granule in flight during the matrixing and window
+    load(g + 1, A);
     wave_sync();
     // ---- matrixing (frame.go:642-648): lane (ch, slot) turns its S row into X ----
     {
@@ -173,21 +231,7 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
     wave_sync();
     // ---- 16-tap window -> s16 PCM (frame.go:649-678); the stores are issued
     //      for replayed granules too, through a resource with no records ----
-    uint32_t pk[9] = {};  // (dropped for replayed granules)
     if (out) {
-#if !MP3G_SYNTH_DW_REGS
-      {
-        const float4* d4 = reinterpret_cast<const float4*>(&dwin_s[k][0]);
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-          const float4 v = d4[q];
-          dw[4 * q] = v.x;
-          dw[4 * q + 1] = v.y;
-          dw[4 * q + 2] = v.z;
-          dw[4 * q + 3] = v.w;
-        }
-      }
-#endif
       const f2* RA = reinterpret_cast<const f2*>(&s.ring[ch][pa][0]);
       const float* RB = &s.ring[ch][pb][0];
       f2 acc2[9];
@@ -195,36 +239,20 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
       for (int p = 0; p < 9; p++) acc2[p] = bcast(0.0f);
 #pragma unroll
       for (int v = -14; v <= 16; v += 2) {
-        const f2 A = RA[(kHist + v) / 2];
-        const f2 B = {RB[kHist + v - 1], RB[kHist + v]};
+        const f2 Av = RA[(kHist + v) / 2];
+        const f2 Bv = {RB[kHist + v - 1], RB[kHist + v]};
 #pragma unroll
         for (int t = 0; t < 8; t++) {
           const int p = v / 2 + t;
           if (p >= 0 && p < 9) {
-            acc2[p] = pfma(bcast(dw[2 * t]), A, acc2[p]);
-            acc2[p] = pfma(bcast(dw[2 * t + 1]), B, acc2[p]);
+            acc2[p] = pfma(bcast(dw[2 * t]), Av, acc2[p]);
+            acc2[p] = pfma(bcast(dw[2 * t + 1]), Bv, acc2[p]);
           }
         }
       }
-      auto pack = [&](auto mono) {
-#pragma unroll
-        for (int p = 0; p < 9; p++) {
-          const int a = (int)__builtin_amdgcn_fmed3f(acc2[p].x, -32767.0f, 32767.0f);
-          const int b = (int)__builtin_amdgcn_fmed3f(acc2[p].y, -32767.0f, 32767.0f);
-          const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
-          pk[p] = __builtin_amdgcn_perm((uint32_t)(decltype(mono)::value ? r[0] : r[1]), (uint32_t)r[0], 0x05040100u);
-        }
-      };
-      if (nch == 2) pack(std::false_type{});
-      else pack(std::true_type{});
+      pack_pcm(acc2, nch, pk);
     }
-    {
-      const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
-          pcm + (size_t)g * 1152, (short)0, out ? MP3G_PCM_BYTES_PER_GRANULE : 0, 0x00020000);
-#pragma unroll
-      for (int p = 0; p < 9; p++)
-        __builtin_amdgcn_raw_buffer_store_b32(pk[p], rp, 4 * (32 * (2 * p + hi) + k), 0, MP3G_SYNTH_STORE_AUX);
-    }
+    store_pcm(pcm, g, out, pk, hi, k);
     wave_sync();
     // ---- history shift of the channels this granule touched ----
     if (ch < nch) {
@@ -233,48 +261,45 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
       for (int q = 0; q < 8; q++) col[q] = col[9 + q];
     }
     wave_sync();
-  };
-
-#if MP3G_SYNTH_DEPTH == 1
-  f2 A[9];
-  load(w, A);
-  wave_sync();
-#if MP3G_SYNTH_PRIO
-  const uint32_t span = end - w, span2 = 2 * span, span3 = 3 * span;
-#endif
-  for (uint32_t g = w; g < end; g++) {
-#if MP3G_SYNTH_PRIO
-    // progress-balanced issue priority, as in the fused kernel
-    const uint32_t left4 = 4u * (end - g);
-    if (left4 > span3) __builtin_amdgcn_s_setprio(3);
-    else if (left4 > span2) __builtin_amdgcn_s_setprio(2);
-    else if (left4 > span) __builtin_amdgcn_s_setprio(1);
-    else __builtin_amdgcn_s_setprio(0);
-#endif
-    granule(g, A);
   }
-#else
-  // two granules in flight: ping-pong buffers, the loop unrolled by two
-  f2 A[9], B[9];
-  load(w, A);
-  load(w + 1, B);
-  wave_sync();
-  for (uint32_t g = w; g < end; g += 2) {
-    granule(g, A);
-    if (g + 1 < end) granule(g + 1, B);
-  }
-#endif
 
-  if (cd.flags & kChunkStateOut) {
-    // vVec out; the IMDCT overlap `store` is not this stage's: passed through
+  // vVec out; the IMDCT overlap `store` is not this stage's: passed through
+  auto export_state = [&]() {
+    if (!(cd.flags & kChunkStateOut)) return;
     mp3g_state* so = state_out + cd.stream;
     const bool have_in = (cd.flags & kChunkStateIn) && sin;
-    for (int e = lane; e < 2 * 32 * 18; e += kLanes)
+    for (int e = lane_fresh(); e < 2 * 32 * 18; e += kLanes)
       (&so->store[0][0][0])[e] = have_in ? (&sin->store[0][0][0])[e] : 0.0f;
-    for (int e = lane; e < 2 * 1024; e += kLanes) {
+    for (int e = lane_fresh(); e < 2 * 1024; e += kLanes) {
       const int c = e >> 10, blk = (e >> 6) & 15, i = e & 63;
       so->vvec[c][64 * blk + i] = blk < 15 ? v_from_x(&s.ring[c][0][kHist - 1 - blk], i) : 0.0f;
     }
+  };
+  export_state();
+
+  // ---- hot zones (rare): redone in the reference's order from their replay
+  //      start, PCM overwritten; a zone reaching the chunk end rewrites the
+  //      exported state (see the fused kernel) ----
+  if (nz) {
+    uint32_t done = 0;
+    bool have = false;
+    for (uint32_t i = 0; i < nz; i++) {
+      const uint32_t zs = __builtin_amdgcn_readfirstlane(s.zone[i][0]);
+      uint32_t ze = __builtin_amdgcn_readfirstlane(s.zone[i][1]);
+      if (have && ze <= done) continue;
+      uint32_t g = done;
+      if (!have || zs > done) {
+        int zin[2];
+        g = synth_replay_start(cd, zs, gran, zin, lane_fresh());
+        synth_init_ring(s, sin, zin, lane_fresh());
+        wave_sync();
+        have = true;
+      }
+      for (; g < ze; g++)
+        if (synth_exact_granule(gran, lines, pcm, s, g, g >= zs)) ze = g + 2 > ze ? (g + 2 < end ? g + 2 : end) : ze;
+      done = g;
+    }
+    if (done >= end) export_state();
   }
 }
 

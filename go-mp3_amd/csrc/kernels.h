@@ -57,7 +57,8 @@ hipError_t launch_fast_stamped(const ChunkDesc* d_chunks, uint32_t n_chunks, con
 
 // The fast kernel's TU (kernels_fast.hip): its table copy, attributes and launch
 // (d_stamps = nullptr: the production build).
-hipError_t upload_fast_tables(const FastTables& fast);
+// (req: DspTables::req, the exact requantization table of the hot-granule fallback)
+hipError_t upload_fast_tables(const FastTables& fast, const float* req);
 hipError_t fast_kernel_attributes(hipFuncAttributes* a, int* waves_per_block);
 hipError_t launch_fast(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_granule* d_gran,
                        const int16_t* d_coef, const mp3g_state* d_state_in, mp3g_state* d_state_out,

@@ -35,7 +35,7 @@ hipError_t upload_tables(const DspTables& tables) {
   if (e != hipSuccess) return e;
   FastTables fast;
   build_fast_tables(tables, &fast);
-  e = upload_fast_tables(fast);
+  e = upload_fast_tables(fast, &tables.req[0][0]);
   if (e != hipSuccess) return e;
   HuffLut* lut = new HuffLut;
   if (!build_huff_lut(lut)) {

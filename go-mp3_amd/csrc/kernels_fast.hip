@@ -19,6 +19,9 @@
 
 namespace mp3g {
 __constant__ FastTables g_fast;
+// DspTables::req (131 KB, global memory): the exact requantization of the
+// reference-order fallback for hot granules (granule_fast.hip)
+__device__ float g_req[4][8207];
 }  // namespace mp3g
 
 #include "granule_hdr.h"
@@ -27,8 +30,10 @@ __constant__ FastTables g_fast;
 
 namespace mp3g {
 
-hipError_t upload_fast_tables(const FastTables& fast) {
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_fast), &fast, sizeof(FastTables), 0, hipMemcpyHostToDevice);
+hipError_t upload_fast_tables(const FastTables& fast, const float* req) {
+  const hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_fast), &fast, sizeof(FastTables), 0, hipMemcpyHostToDevice);
+  if (e != hipSuccess) return e;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_req), req, sizeof(float) * 4 * 8207, 0, hipMemcpyHostToDevice);
 }
 
 hipError_t fast_kernel_attributes(hipFuncAttributes* a, int* waves_per_block) {

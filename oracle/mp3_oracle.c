@@ -1178,6 +1178,33 @@ void orc_hybrid_streams(const mp3g_granule* g, const int16_t* coef, const mp3g_s
   }
 }
 
+/* requantize .. antialias (frame.go:121-131 up to antialias, :140-452): no
+ * state crosses granules before the IMDCT, so each granule stands alone. */
+void orc_frontend_granules(const mp3g_granule* g, const int16_t* coef, size_t n, float* xr_out) {
+  ensure_init();
+  for (size_t k = 0; k < n; k++) {
+    gc_fields c[2];
+    float is[2][576];
+    memset(c, 0, sizeof c);
+    const uint32_t h = g[k].header;
+    const int nch = fh_nch(h);
+    for (int ch = 0; ch < 2; ch++) {
+      fields_from_desc(&g[k].ch[ch], &c[ch]);
+      for (int i = 0; i < 576; i++) is[ch][i] = (float)coef[k * 1152 + ch * 576 + i];
+    }
+    const int* sl = SFB_LONG[fh_lsf(h)][fh_sfreq(h)];
+    const int* ss = SFB_SHORT[fh_lsf(h)][fh_sfreq(h)];
+    for (int ch = 0; ch < nch; ch++) {
+      dsp_requantize(&c[ch], sl, ss, is[ch]);
+      dsp_reorder(&c[ch], ss, is[ch]);
+    }
+    dsp_stereo(h, c, sl, ss, is);
+    for (int ch = 0; ch < nch; ch++) dsp_antialias(&c[ch], is[ch]);
+    if (nch == 1) memset(is[1], 0, sizeof is[1]);
+    memcpy(xr_out + k * 1152, is, sizeof is);
+  }
+}
+
 /* subbandSynthesis alone (frame.go:630-688) over streams of granules whose
  * frequency-inverted lines are given as float32 [n][2][576]: the semantics of
  * mp3g_plan_synth_execute.  state: vvec carried per stream (flags as

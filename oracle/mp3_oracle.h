@@ -78,6 +78,10 @@ int orc_dsp_streams(const mp3g_granule* g, const int16_t* coef, const mp3g_strea
  * float32 lines [n][2][576] as subbandSynthesis reads them (test inputs). */
 void orc_hybrid_streams(const mp3g_granule* g, const int16_t* coef, const mp3g_stream* streams,
                         uint32_t n_streams, const mp3g_state* state_in, float* is_out);
+/* The stateless front end only (requantize, reorder, stereo, antialias;
+ * frame.go:140-452): the float32 lines the IMDCT reads, [n][2][576]
+ * (mono: [g][1][*] = 0).  Test / analysis input (magnitude thresholds). */
+void orc_frontend_granules(const mp3g_granule* g, const int16_t* coef, size_t n, float* xr_out);
 /* subbandSynthesis alone (frame.go:630-688): the semantics of
  * mp3g_plan_synth_execute (vvec carried; store passed through). */
 int orc_synth_streams(const mp3g_granule* g, const float* is, const mp3g_stream* streams,

@@ -62,6 +62,7 @@ def lib():
         L.orc_dsp_streams.argtypes = [vp, vp, vp, C.c_uint32, vp, vp, vp]
         L.orc_dsp_streams_mt.argtypes = [vp, vp, vp, C.c_uint32, vp, C.c_int]
         L.orc_hybrid_streams.argtypes = [vp, vp, vp, C.c_uint32, vp, vp]
+        L.orc_frontend_granules.argtypes = [vp, vp, sz, vp]
         L.orc_synth_streams.argtypes = [vp, vp, vp, C.c_uint32, vp, vp, vp]
         L.orc_tables.argtypes = [vp] * 6
         L.orc_bits_read.argtypes = [vp, sz, vp, C.c_int, vp, vp]
@@ -131,6 +132,16 @@ def hybrid_streams(granules, coeffs, streams, state_in=None):
     if state_in is None:
         state_in = np.zeros(len(streams), STATE_DTYPE)
     L.orc_hybrid_streams(_ptr(granules), _ptr(coeffs), _ptr(streams), len(streams), _ptr(state_in), _ptr(out))
+    return out
+
+
+def frontend_granules(granules, coeffs):
+    """requantize .. antialias (frame.go:140-452): float32 lines [n, 2, 576] the IMDCT reads."""
+    L = lib()
+    granules = np.ascontiguousarray(granules, dtype=GRANULE_DTYPE)
+    coeffs = np.ascontiguousarray(coeffs, dtype=np.int16)
+    out = np.zeros((len(granules), 2, 576), np.float32)
+    L.orc_frontend_granules(_ptr(granules), _ptr(coeffs), len(granules), _ptr(out))
     return out
 
 

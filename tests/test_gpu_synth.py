@@ -107,13 +107,74 @@ def test_synth_silence_and_clipping(gpu):
     pcm, _ = run_synth(gpu, g, zeros, s)
     assert not pcm.any()
     # a loud low-frequency tone: subband 0 of both channels at 4.0 (PCM far
-    # past full scale without the cancellation of huge alternating values)
+    # past full scale)
     loud = np.zeros((len(g), 2, 576), np.float32)
     loud[:, :, :18] = 4.0
     want, _ = oracle.synth_streams(g, loud, s)
     got, _ = run_synth(gpu, g, loud, s)
     assert_close(got, want, "clipping")
     assert np.abs(got.astype(np.int32)).max() == 32767
+    # lines of +-1e4 with alternating signs: huge values whose windowed sums
+    # cancel to mid-range PCM -- the reference's own float32 rounding decides
+    # the PCM, so these granules run in the reference's order (hot zones)
+    loud = np.full((len(g), 2, 576), 1e4, np.float32)
+    loud[:, :, 1::2] *= -1
+    want, _ = oracle.synth_streams(g, loud, s)
+    got, _ = run_synth(gpu, g, loud, s)
+    assert_close(got, want, "alternating +-1e4")
+
+
+def hot_lines(rng, n, kind, scale):
+    i = np.arange(576)
+    if kind == "alt":
+        L = np.where(i % 2 == 0, scale, -scale) * np.ones((n, 2, 1))
+    elif kind == "altsb":
+        L = np.where((i // 18) % 2 == 0, scale, -scale) * np.ones((n, 2, 1))
+    elif kind == "randsign":
+        L = rng.choice([-1.0, 1.0], size=(n, 2, 576)) * scale
+    else:
+        L = rng.standard_normal((n, 2, 576)) * scale / (1.0 + i / 64.0)
+    return L.astype(np.float32)
+
+
+@pytest.mark.parametrize("kind", ["alt", "altsb", "randsign", "gauss"])
+def test_synth_hot_granules(gpu, kind):
+    """Granules far above the fast transforms' magnitude bound (kHotS = 8)
+    scattered through normal ones, isolated and in runs, at chunk starts and
+    stream ends: max |dPCM| <= 1 against the oracle, bit-identical across
+    chunkings, exported vVec close to the reference's."""
+    rng = np.random.default_rng(len(kind))
+    g, c, s = synth.synth_batch(3, 40, seed=77)
+    s = gpu.streams_for([80, 80, 80], gpu.STATE_OUT)
+    lines = oracle.hybrid_streams(g, c, s)
+    hot = np.zeros(len(g), bool)
+    hot[[0, 5, 17, 18, 19, 40, 79, 80, 81, 150, 200, 238, 239]] = True
+    lines[hot] = hot_lines(rng, int(hot.sum()), kind, 1e4 if kind != "gauss" else 300.0)
+    want, so_ref = oracle.synth_streams(g, lines, s)
+    serial, so_serial = run_synth(gpu, g, lines, s, chunk=80)
+    assert_close(serial, want, f"{kind} serial")
+    # (a zone that reaches a stream's end exports the reference-order state)
+    for st in range(3):
+        scale = max(1.0, float(np.abs(so_ref["vvec"][st]).max()))
+        np.testing.assert_allclose(so_serial["vvec"][st, :, :960], so_ref["vvec"][st, :, :960], rtol=0,
+                                   atol=2e-5 * scale)
+    for chunk in (1, 2, 3, 7, 0):
+        pcm, so = run_synth(gpu, g, lines, s, chunk=chunk)
+        assert np.array_equal(pcm, serial), f"{kind} chunk={chunk} differs from the serial run"
+        assert so.tobytes() == so_serial.tobytes(), f"{kind} chunk={chunk}: exported state differs"
+
+
+@pytest.mark.parametrize("kind", ["alt", "altsb", "randsign", "gauss"])
+def test_synth_just_below_bound(gpu, kind):
+    """At 0.95 x the bound every granule stays on the fast transforms: the
+    +-1 LSB margin the bound is placed for."""
+    rng = np.random.default_rng(100 + len(kind))
+    g, c, s = synth.synth_batch(4, 60, seed=91)
+    lines = hot_lines(rng, len(g), kind, 1.0)
+    lines *= 0.95 * 8.0 / np.abs(lines).max(axis=(1, 2), keepdims=True)
+    want, _ = oracle.synth_streams(g, lines, s)
+    got, _ = run_synth(gpu, g, lines, s)
+    assert_close(got, want, f"{kind} at 0.95 kHotS")
 
 
 def test_synth_empty_plan_and_errors(gpu):
