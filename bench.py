@@ -4,9 +4,12 @@
 metric : MP3 frames/sec (44.1 kHz stereo 128 kbps) at 1/2/4/8 GPUs; max |dPCM| LSB
 step   : one launch of the device plan over one batch of device-resident
          boundary input (granule descriptors + int16 coefficients) -> s16 PCM.
-workload (default, --config c2 = BASELINE configs[1]): one 44.1 kHz stereo
-         128 kbps CBR stream of 10,000 frames per GPU, granule-parallel
-         (chunks + 2-granule halo).  --config c3: 1,024 streams x 1,024 frames.
+workload (default, --config c3 = BASELINE configs[2], the largest single-GPU
+         config and c4's per-GPU shard): 1,024 independently seeded 44.1 kHz
+         stereo 128 kbps CBR streams x 1,024 frames per GPU (seeds
+         1 + 1024 rank .. 1024 (rank + 1), synthetic Layer III writer); the c2
+         stream (1 x 10,000 frames, granule-parallel) is timed beside it.
+         --config c2 / c5: those configs as the headline.
 scaling: weak -- every rank decodes its own stream(s); no data-path collective
          (value = frames of all ranks / max-over-ranks time).  --gather adds a
          separately reported RCCL gather of the PCM to rank 0.
@@ -42,7 +45,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", choices=["c2", "c3", "c5"], default="c2")
+    ap.add_argument("--config", choices=["c2", "c3", "c5"], default="c3")
     ap.add_argument("--c5-copies", type=int, default=256,
                     help="c5: copies of each reference sample stream per GPU")
     ap.add_argument("--chunk", type=int, default=0, help="granules per chunk (0 = auto)")
@@ -60,6 +63,9 @@ def parse():
                          "kernel launch then has the timed launches' size)")
     ap.add_argument("--no-polyphase", action="store_true",
                     help="skip the standalone polyphase kernel leg (mp3g_plan_synth_execute)")
+    ap.add_argument("--no-c2", action="store_true", help="c3: skip the secondary c2 object")
+    ap.add_argument("--parity-streams", type=int, default=128,
+                    help="c3: streams whose PCM is checked against the oracle (all host threads)")
     return ap.parse_args()
 
 
@@ -86,16 +92,22 @@ def build_workload(cfg, rank, seed_base=1, c5_copies=256):
         return g, c, s, {"workload": "c2: 1 stream x 10,000 frames, 44.1 kHz stereo 128 kbps CBR "
                                      "(synthetic boundary input), granule-parallel",
                          "streams_per_gpu": 1, "frames_per_stream": 10000}
-    # c3: 1024 streams x 1024 frames, descriptors tiled from a seeded pool
-    pg, pc, idx, s = synth.synth_pool_batch(1024, 1024, seed=seed_base + 1000003 * rank,
-                                           pool_frames=8192)
-    return (pg, pc, idx), None, s, {"workload": "c3: 1,024 streams x 1,024 frames, 44.1 kHz stereo "
-                                                "128 kbps CBR (synthetic; descriptors tiled from a "
-                                                "16,384-granule seeded pool)",
-                                    "streams_per_gpu": 1024, "frames_per_stream": 1024}
+    # c3: 1,024 independently seeded streams x 1,024 frames;
+    # rank r takes seeds 1 + 1024 r .. 1024 (r + 1), so N ranks decode c4's
+    # N x 1,024 distinct streams.  Real Layer III bitstreams from the
+    # synthetic writer; the boundary input is the writer's own record of
+    # them (byte-identical to what the host parse recovers, tests/test_gpu_huffman.py)
+    t = time.perf_counter()
+    datas, g, c, s = synth.encode_batch(range(seed_base + 1024 * rank, seed_base + 1024 * (rank + 1)), 1024,
+                                        n_threads=16)
+    return g, c, s, {"workload": "c3: 1,024 independently seeded streams x 1,024 frames, 44.1 kHz stereo "
+                                 "128 kbps CBR (synthetic Layer III writer, seeds %d..%d)"
+                                 % (seed_base + 1024 * rank, seed_base + 1024 * (rank + 1) - 1),
+                     "streams_per_gpu": 1024, "frames_per_stream": 1024,
+                     "writer_s": round(time.perf_counter() - t, 2), "bitstreams": datas}
 
 
-def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle, pipelined=True):
+def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle, pipelined=True, datas=None):
     """the same workload as real Layer III bitstreams
     (synthetic writer, go-mp3_amd/csrc/synth_enc.cpp): host scan (headers,
     side info, reservoir) on 16 threads, then on device-resident input the
@@ -109,8 +121,9 @@ def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle, pip
     n_streams, n_frames = (1, 10000) if cfg == "c2" else (1024, 1024)
     seed0 = 1 + 1000003 * rank
     t = time.perf_counter()
-    with ThreadPoolExecutor(16) as ex:  # the writer releases the GIL (ctypes)
-        datas = list(ex.map(lambda k: synth.encode_stream(seed0 + k, n_frames), range(n_streams)))
+    if datas is None:
+        with ThreadPoolExecutor(16) as ex:  # the writer releases the GIL (ctypes)
+            datas = list(ex.map(lambda k: synth.encode_stream(seed0 + k, n_frames), range(n_streams)))
     writer_s = time.perf_counter() - t
     s = mp3g.scan_streams(datas, n_threads=16)
     scan_s = s["scan_s"]  # the library call alone (not the numpy copies of its buffers)
@@ -266,7 +279,7 @@ def polyphase_leg(args, rank, dev, stream, d_g, streams, n_gran, local):
     ms = ev0.elapsed_time(ev1) / args.steps
     n_gc = 2 * n_gran  # c2 / c3 are stereo throughout
     achieved = n_gc * POLY_BYTES_PER_GC / (ms * 1e-3) / 1e9
-    traffic, traffic_src = profiled_traffic(args.config, "granule_synth_kernel")
+    traffic, traffic_src, _ = profiled_traffic(args.config, "granule_synth_kernel")
     out = {"kernel": "mp3g::v3::granule_synth_kernel", "entry": "mp3g_plan_synth_execute",
            "kernel_ms": round(ms, 4), "granule_channels_per_s": round(n_gc / (ms * 1e-3), 1),
            "frames_per_s": round(n_gran / 2 / (ms * 1e-3), 1),
@@ -275,25 +288,30 @@ def polyphase_leg(args, rank, dev, stream, d_g, streams, n_gran, local):
                         "traffic_source": traffic_src, "algorithmic_bytes_per_gc": POLY_BYTES_PER_GC,
                         "algorithmic_bytes_per_launch": n_gc * POLY_BYTES_PER_GC},
            "input": "synthetic float32 frequency-inverted lines [n][2][576], device-resident"}
-    if rank == 0 and args.config == "c2" and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import oracle  # checker of the timed output only
-        g_host = d_g.cpu().numpy().view(mp3g.GRANULE_DTYPE)
-        lines = d_lines.cpu().numpy()
-        ref, _ = oracle.synth_streams(g_host, lines, streams)
-        got = d_pcm.cpu().numpy().reshape(-1, 576, 2)
+        # c2: the whole stream; c3: its first 16 streams
+        n_chk = n_gran if args.config == "c2" else min(n_gran, 16 * int(streams["n_granules"][0]))
+        s_chk = streams if args.config == "c2" else mp3g.streams_for([int(streams["n_granules"][0])] * 16)
+        g_host = d_g[:n_chk * 160].cpu().numpy().view(mp3g.GRANULE_DTYPE)
+        lines = d_lines[:n_chk].cpu().numpy()
+        ref, _ = oracle.synth_streams(g_host, lines, s_chk)
+        got = d_pcm[:n_chk * 1152].cpu().numpy().reshape(-1, 576, 2)
         out["max_dpcm_lsb"] = int(np.abs(got.astype(np.int32) - ref.astype(np.int32)).max())
+        out["parity_granules"] = int(n_chk)
     del d_lines, d_pcm
     return out
 
 
-PROFILE_TAG = "r02i"  # profiles/<tag>_<cfg>_<kernel>.json of the current kernels
+PROFILE_TAG = "r03"  # profiles/<tag>_<cfg>_<kernel>.json of the current kernels
 
 
 def profiled_traffic(cfg, kernel):
     """HBM bytes per launch from the newest rocprofv3 PMC summary in profiles/
     for this config and kernel (FETCH_SIZE x2 + WRITE_SIZE, KiB -> B;
-    tools/summarize_profile.py), or None."""
+    tools/summarize_profile.py), its path and the library build it profiled
+    (sha256 prefix, or None), or (None, None, None)."""
     import glob
     files = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_{cfg}*.json")))
     # the current profile set first, then older ones (newest name last)
@@ -302,8 +320,69 @@ def profiled_traffic(cfg, kernel):
     for f in reversed(files):
         d = json.load(open(f))
         if kernel in d.get("kernel", "") and d.get("hbm_bytes_per_launch_corrected"):
-            return d["hbm_bytes_per_launch_corrected"], os.path.relpath(f, REPO)
-    return None, None
+            return d["hbm_bytes_per_launch_corrected"], os.path.relpath(f, REPO), d.get("lib_sha16")
+    return None, None, None
+
+
+def host_info():
+    """The box's CPU as the CPU baseline ran on it."""
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = None
+    return {"nproc": os.cpu_count(), "affinity_cpus": affinity, "cpu_model": model,
+            "threads_used": CPU_THREADS,
+            "note": "nproc is the whole machine; this job's CPU share on the GPU box is 16 threads"}
+
+
+CPU_THREADS = 16  # the GPU box's CPU share per GPU
+
+
+def lib_sha16():
+    import hashlib
+    import mp3g
+    return hashlib.sha256(open(mp3g.lib_path(), "rb").read()).hexdigest()[:16]
+
+
+def time_plan(mp3g, streams, d_g, d_c, d_pcm, mode, chunk, local, steps, warmup, stream, world, dev):
+    """W untimed + K timed launches of one plan; barrier + synchronize on both
+    sides of the timed region; HIP events on the launch stream."""
+    import torch
+    import torch.distributed as dist
+    h = stream.cuda_stream
+    plan = mp3g.Plan(streams, granules_per_chunk=chunk, mode=mode, device=local)
+    pinfo = plan.info()
+    for _ in range(warmup):
+        plan.execute(d_g, d_c, d_pcm, stream=h)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(steps):
+        plan.execute(d_g, d_c, d_pcm, stream=h)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    plan.close()
+    return wall, ev0.elapsed_time(ev1) / steps, pinfo
+
+
+def dpcm(a, b):
+    return int(np.abs(a.astype(np.int32) - b.astype(np.int32)).max(initial=0))
 
 
 def main():
@@ -322,19 +401,10 @@ def main():
     from mp3g import dist as mdist
 
     g, c, streams, cfg_info = build_workload(args.config, rank, c5_copies=args.c5_copies)
-    if args.config == "c3":
-        pg, pc, idx = g
-        d_pool_g = torch.from_numpy(pg.view(np.uint8).reshape(len(pg), -1).copy()).to(dev)
-        d_pool_c = torch.from_numpy(pc.reshape(len(pc), -1).copy()).to(dev)
-        d_idx = torch.from_numpy(idx).to(dev)
-        d_g = d_pool_g.index_select(0, d_idx).reshape(-1).contiguous()
-        d_c = d_pool_c.index_select(0, d_idx).reshape(-1).contiguous()
-        del d_pool_g, d_pool_c
-        n_gran = len(idx)
-    else:
-        d_g = torch.from_numpy(g.view(np.uint8).copy()).to(dev)
-        d_c = torch.from_numpy(c.reshape(-1).copy()).to(dev)
-        n_gran = len(g)
+    datas = cfg_info.pop("bitstreams", None)
+    d_g = torch.from_numpy(g.view(np.uint8).copy()).to(dev)
+    d_c = torch.from_numpy(c.reshape(-1)).to(dev)
+    n_gran = len(g)
     if args.config == "c5":  # MPEG-1 frames are two granules, MPEG-2 LSF frames one
         lsf = ((g["header"] >> 19) & 3) != 3
         n_frames = int(lsf.sum() + (~lsf).sum() // 2)
@@ -345,34 +415,14 @@ def main():
     h = stream.cuda_stream
 
     def measure(mode_name):
-        """W untimed + K timed launches of one plan; barrier + synchronize on
-        both sides of the timed region, max over ranks."""
         mode = mp3g.MODE_FAST if mode_name == "fast" else mp3g.MODE_EXACT
-        plan = mp3g.Plan(streams, granules_per_chunk=args.chunk, mode=mode, device=local)
-        pinfo = plan.info()
-        for _ in range(args.warmup):
-            plan.execute(d_g, d_c, d_pcm, stream=h)
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        t0 = time.perf_counter()
-        ev0.record(stream)
-        for _ in range(args.steps):
-            plan.execute(d_g, d_c, d_pcm, stream=h)
-        ev1.record(stream)
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        wall = time.perf_counter() - t0
-        kern_ms = ev0.elapsed_time(ev1) / args.steps  # HIP events on the launch stream
+        wall, kern_ms, pinfo = time_plan(mp3g, streams, d_g, d_c, d_pcm, mode, args.chunk, local, args.steps,
+                                         args.warmup, stream, world, dev)
         t_max = mdist.max_over_ranks(wall, device=dev)
-        plan.close()
         frames_all = n_frames * world
         return {"value": frames_all * args.steps / t_max, "ms_per_step": 1000.0 * t_max / args.steps,
                 "kernel_ms": kern_ms, "chunks": pinfo["chunks"], "halo_granules": pinfo["halo_granules"],
+                # (rank 0) the timed output, for the parity check below
                 "pcm": d_pcm.cpu().numpy().reshape(-1, 576, 2) if rank == 0 else None}
 
     modes = [args.mode] + ([] if args.single_mode else [m for m in MODES if m != args.mode])
@@ -385,11 +435,37 @@ def main():
         bitstream = bitstream_leg(args.config, rank, dev, stream,
                                   mp3g.MODE_FAST if args.mode == "fast" else mp3g.MODE_EXACT,
                                   args.steps, args.warmup, check_oracle=rank == 0 and args.config == "c2",
-                                  pipelined=not args.no_pipelined)
+                                  pipelined=not args.no_pipelined, datas=datas)
 
     polyphase = None
     if not args.no_polyphase and args.config in ("c2", "c3"):
         polyphase = polyphase_leg(args, rank, dev, stream, d_g, streams, n_gran, local)
+
+    # the c2 stream beside the c3 headline (BASELINE configs[1]; granule-parallel)
+    c2 = None
+    if args.config == "c3" and not args.no_c2:
+        g2, c2c, s2, _ = build_workload("c2", rank)
+        d_g2 = torch.from_numpy(g2.view(np.uint8).copy()).to(dev)
+        d_c2 = torch.from_numpy(c2c.reshape(-1)).to(dev)
+        d_p2 = torch.empty(len(g2) * 1152, dtype=torch.int16, device=dev)
+        wall, kern_ms, pinfo = time_plan(mp3g, s2, d_g2, d_c2, d_p2, mp3g.MODE_FAST, 0, local, max(args.steps, 20),
+                                         args.warmup, stream, world, dev)
+        steps2 = max(args.steps, 20)
+        t_max = mdist.max_over_ranks(wall, device=dev)
+        c2 = {"workload": "c2: 1 stream x 10,000 frames, 44.1 kHz stereo 128 kbps CBR (synthetic boundary input), "
+                          "granule-parallel", "mode": MODES["fast"][0],
+              "value": round(len(g2) // 2 * world * steps2 / t_max, 1), "ms_per_step": round(1000 * t_max / steps2, 4),
+              "kernel_ms": round(kern_ms, 4), "chunks": pinfo["chunks"], "halo_granules": pinfo["halo_granules"],
+              "roofline": {"achieved": round(len(g2) * BYTES_PER_GRANULE / (kern_ms * 1e-3) / 1e9, 2),
+                           "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                           "frac": round(len(g2) * BYTES_PER_GRANULE / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5),
+                           "note": "95 MB per launch: Infinity-Cache resident, not an HBM figure"}}
+        if rank == 0 and not args.no_cpu_baseline:
+            sys.path.insert(0, os.path.join(REPO, "oracle"))
+            import oracle  # checker of the timed output only
+            ref2 = oracle.dsp_streams_mt(g2, c2c, s2, 1)
+            c2["max_dpcm_lsb"] = dpcm(d_p2.cpu().numpy().reshape(-1, 576, 2), ref2)
+        del d_g2, d_c2, d_p2
 
     gather_ms = None
     if args.gather and world > 1:
@@ -403,7 +479,7 @@ def main():
     if rank == 0:
         kern_ms = main_res["kernel_ms"]
         achieved = n_gran * BYTES_PER_GRANULE / (kern_ms * 1e-3) / 1e9
-        traffic, traffic_src = profiled_traffic(args.config, MODES[args.mode][1])
+        traffic, traffic_src, traffic_sha = profiled_traffic(args.config, MODES[args.mode][1])
         out = {
             "metric": METRIC,
             "value": round(main_res["value"], 1),
@@ -427,51 +503,75 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
                          "traffic": traffic, "traffic_source": traffic_src,
+                         "traffic_same_build": None if traffic_sha is None else traffic_sha == lib_sha16(),
                          "kernel": MODES[args.mode][1], "kernel_ms": round(kern_ms, 4),
                          "algorithmic_bytes_per_frame": BYTES_PER_FRAME,
                          "algorithmic_bytes_per_launch": n_gran * BYTES_PER_GRANULE},
             "modes": {m: {"value": round(r["value"], 1), "kernel_ms": round(r["kernel_ms"], 4),
                           "kernel": MODES[m][1], "pcm": MODES[m][0]} for m, r in res.items()},
         }
+        if out["roofline"]["traffic_same_build"] is False:
+            print("bench.py: warning: roofline traffic is from a profile of another build (%s)" % traffic_src,
+                  file=sys.stderr)
         if gather_ms is not None:
             out["gather_ms"] = round(gather_ms, 3)
         if bitstream is not None:
             out["bitstream"] = bitstream
         if polyphase is not None:
             out["polyphase"] = polyphase
-        if world == 1 and not args.no_cpu_baseline and args.config == "c2":
+        if c2 is not None:
+            out["c2"] = c2
+        if world == 1 and not args.no_cpu_baseline and args.config in ("c2", "c3"):
             sys.path.insert(0, os.path.join(REPO, "oracle"))
             import oracle  # CPU baseline leg + parity check of the timed output
+            per = 2 * cfg_info["frames_per_stream"]
+            if args.config == "c2":
+                sample, sample_streams = (g, c, streams), 1
+            else:  # a bounded sample of the same workload: its first 8 streams
+                sample_streams = 8
+                ss = mp3g.streams_for([per] * sample_streams)
+                sample = (g[:per * sample_streams], c[:per * sample_streams], ss)
             times = []
-            ref = None
-            for _ in range(args.cpu_repeats):
+            for _ in range(args.cpu_repeats if args.config == "c2" else 3):
                 t = time.perf_counter()
-                ref, _ = oracle.dsp_streams(g, c, streams)
+                oracle.dsp_streams_mt(*sample, 1)
                 times.append(time.perf_counter() - t)
-            cpu_fps = frames_rank / float(np.median(times))
-            out["cpu_baseline"] = {"value": round(cpu_fps, 1), "unit": "frames/s", "cores": 1,
-                                   "kind": "port",
-                                   "sample": f"full c2 stream ({frames_rank} frames), oracle C "
-                                             f"restatement -O2 -ffp-contract=off, 1 thread, median "
-                                             f"of {args.cpu_repeats}"}
-            # all host cores of this rank's share (16 on the GPU box): the c2
-            # stream's granules as 16 independent streams, one per thread
-            reps = 16
-            gm, cm = np.concatenate([g] * reps), np.concatenate([c] * reps)
-            sm = mp3g.streams_for([len(g)] * reps)
-            t = time.perf_counter()
-            oracle.dsp_streams_mt(gm, cm, sm, reps)
-            out["cpu_baseline_all_cores"] = {
-                "value": round(frames_rank * reps / (time.perf_counter() - t), 1), "unit": "frames/s",
-                "cores": reps, "kind": "port",
-                "sample": f"{reps} copies of the c2 stream, one per thread (oracle, -O2 -ffp-contract=off)"}
+            sample_frames = len(sample[0]) // 2
+            out["cpu_baseline"] = {"value": round(sample_frames / float(np.median(times)), 1), "unit": "frames/s",
+                                   "cores": 1, "kind": "port",
+                                   "sample": f"{sample_streams} stream(s) x {sample_frames // sample_streams} frames "
+                                             f"of this workload, oracle C restatement -O2 -ffp-contract=off, "
+                                             f"1 thread, median of {len(times)}",
+                                   "host": host_info()}
+            # parity of the timed output: the oracle on the first
+            # --parity-streams streams (c2: the stream), all host threads --
+            # which is also the all-cores CPU baseline
+            if args.config == "c2":
+                reps = CPU_THREADS
+                gm, cm = np.concatenate([g] * reps), np.concatenate([c] * reps)
+                t = time.perf_counter()
+                oracle.dsp_streams_mt(gm, cm, mp3g.streams_for([len(g)] * reps), reps)
+                t_all = time.perf_counter() - t
+                ref, _ = oracle.dsp_streams(g, c, streams)
+                n_chk, par_frames = len(g), n_frames * reps
+                sample_all = f"{reps} copies of the c2 stream, one per thread"
+            else:
+                k = min(args.parity_streams, len(streams))
+                n_chk = per * k
+                t = time.perf_counter()
+                ref = oracle.dsp_streams_mt(g[:n_chk], c[:n_chk], mp3g.streams_for([per] * k), CPU_THREADS)
+                t_all = time.perf_counter() - t
+                par_frames = n_chk // 2
+                sample_all = f"the first {k} streams (the parity sample), {CPU_THREADS} threads"
+            out["cpu_baseline_all_cores"] = {"value": round(par_frames / t_all, 1), "unit": "frames/s",
+                                             "cores": CPU_THREADS, "kind": "port",
+                                             "sample": sample_all + " (oracle, -O2 -ffp-contract=off)"}
             for m, r in res.items():
-                d = int(np.abs(r["pcm"].astype(np.int32) - ref.astype(np.int32)).max())
-                out["modes"][m]["max_dpcm_lsb"] = d
+                out["modes"][m]["max_dpcm_lsb"] = dpcm(r["pcm"][:n_chk], ref)
+                out["modes"][m]["parity_granules"] = int(n_chk)
             out["max_dpcm_lsb"] = out["modes"][args.mode]["max_dpcm_lsb"]
         if world == 1 and args.config == "c5":
             # end to end on this box: host parse (all cores) + H2D + decode + D2H
-            import torch
             hg = torch.from_numpy(g.view(np.uint8).copy()).pin_memory()
             hc = torch.from_numpy(c.reshape(-1).copy()).pin_memory()
             hp = torch.empty(n_gran * 1152, dtype=torch.int16).pin_memory()
@@ -515,7 +615,7 @@ def main():
             import oracle  # parity check of the timed output (checker only)
             ref = oracle.dsp_streams_mt(g, c, streams, 16)
             for m, r in res.items():
-                out["modes"][m]["max_dpcm_lsb"] = int(np.abs(r["pcm"].astype(np.int32) - ref.astype(np.int32)).max())
+                out["modes"][m]["max_dpcm_lsb"] = dpcm(r["pcm"], ref)
             out["max_dpcm_lsb"] = out["modes"][args.mode]["max_dpcm_lsb"]
         print(json.dumps(out), flush=True)
     if world > 1:

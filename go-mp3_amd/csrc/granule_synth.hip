@@ -117,9 +117,10 @@ __device__ __forceinline__ bool synth_exact_granule(const mp3g_granule* __restri
   const int nch = hdr_nch(__builtin_amdgcn_readfirstlane(gran[g].header));
   f2 buf[9];
   synth_load(lines, g, nch * 2304u, lane, buf);
-  const bool hot = __builtin_amdgcn_ballot_w64(max_abs_pairs(buf) > kHotS) != 0;
+  const bool hot1 = __builtin_amdgcn_ballot_w64(max_abs_pairs(buf) > kHotS) != 0;
   synth_stage(s, buf, nch);
   wave_sync();
+  const bool hot = hot1 && slot_sums_hot(s.ring, nch);
   if (ch < nch && (lane & 31) < 18) matrix_exact(&s.ring[ch][0][kHist + (lane & 31)]);
   wave_sync();
   uint32_t pk[9] = {};
@@ -208,12 +209,17 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
     const bool out = g >= out_first;
     // a hot granule: its zone is redone in the reference's order after the pass
 #if MP3G_HOT_CHECK
-    if (__builtin_amdgcn_ballot_w64(max_abs_pairs(A) > kHotS)) record_hot(s, nz, g, out_first, end);
+    const bool hot1 = __builtin_amdgcn_ballot_w64(max_abs_pairs(A) > kHotS) != 0;
 #endif
     synth_stage(s, A, nch);
     // the next granule in flight during the matrixing and window
     load(g + 1, A);
     wave_sync();
+#if MP3G_HOT_CHECK
+    // a hot granule (two tests, the second rare and on the staged S): its
+    // zone is redone in the reference's order after the pass
+    if (hot1 && slot_sums_hot(s.ring, nch)) record_hot(s, nz, g, out_first, end);
+#endif
     // ---- matrixing (frame.go:642-648): lane (ch, slot) turns its S row into X ----
     {
       const int slot = lane & 31;

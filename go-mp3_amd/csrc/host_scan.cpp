@@ -559,6 +559,9 @@ int mp3g_decode_streams_into(int device, uint32_t n_streams, const uint8_t* cons
         if (n < pg[k]) {  // ended early: the rest of its range decodes nothing
           holes = true;
           std::memset(static_cast<void*>(j + 2 * n), 0, (size_t)(2 * (pg[k] - n)) * sizeof(mp3g_hjob));
+          // and its granule records hold no stale data of an earlier group
+          // (the Huffman kernel visits them as jobs without scale factors)
+          std::memset(static_cast<void*>(g + n), 0, (size_t)(pg[k] - n) * sizeof(mp3g_granule));
         }
         local[k - k0] = {g_at[k] - G0, (uint32_t)n, 0};
         streams[k].n_granules = (uint32_t)n;

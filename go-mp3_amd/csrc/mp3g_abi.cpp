@@ -271,6 +271,10 @@ int mp3g_plan_create(int device, const mp3g_stream* streams, uint32_t n_streams,
     for (uint32_t s = 0; s < n_streams; s++)
       nc[s] = (streams[s].n_granules + granules_per_chunk - 1) / granules_per_chunk;
   }
+  // ChunkDesc::n_out is 32-bit: a stream cut into too few chunks is refused
+  for (uint32_t s = 0; s < n_streams; s++)
+    if (streams[s].n_granules && (nc[s] == 0 || (streams[s].n_granules + nc[s] - 1) / nc[s] >= (1ull << 32)))
+      return fail(MP3G_ERR_UNSUPPORTED, "chunk of >= 2^32 granules");
   mp3g_plan* p = new (std::nothrow) mp3g_plan;
   if (!p) return fail(MP3G_ERR_OUT_OF_MEMORY, "plan");
   p->device = device;

@@ -40,6 +40,8 @@ assert STREAM_DTYPE.itemsize == 16 and STATE_DTYPE.itemsize == 12800
 
 MODE_EXACT, MODE_FAST, FLAG_CHECKED, FLAG_KERNEL_V1, FLAG_HOST_HUFFMAN = 0, 1, 0x100, 0x200, 0x400
 STATE_IN, STATE_OUT = 1, 2
+MP3G_PCM_BYTES_PER_GRANULE = 2304  # include/mp3g.h: 576 stereo s16 samples
+
 STATUS = {0: "ok", 1: "invalid argument", 2: "invalid granule", 3: "no device", 4: "device error",
           5: "out of memory", 6: "parse error", 7: "eof", 8: "unsupported", 9: "no Xing/Info header",
           10: "unexpected EOF"}
@@ -366,21 +368,43 @@ def decode_streams(datas, mode=MODE_EXACT, n_threads=0, device=0):
     return _take(pcm, k, np.int16, (k, 576, 2)), streams, status[:len(datas)]
 
 
+def _host_buffer(out, want_int16):
+    """(pointer, size in bytes) of a caller's writable, C-contiguous HOST
+    buffer -- a numpy array or a CPU torch tensor (pinned or not).  The
+    library writes host memory through the pointer, so device tensors,
+    non-contiguous views and read-only arrays are refused, and so is any
+    dtype but int16 where the PCM is addressed in samples."""
+    if hasattr(out, "data_ptr"):  # torch.Tensor
+        if out.device.type != "cpu":
+            raise ValueError("output buffer must be in host memory (got a %s tensor)" % out.device)
+        if not out.is_contiguous():
+            raise ValueError("output buffer must be contiguous")
+        if want_int16 and str(out.dtype) != "torch.int16":
+            raise ValueError("output buffer must be int16 (got %s)" % out.dtype)
+        return out.data_ptr(), out.numel() * out.element_size()
+    a = out
+    if not isinstance(a, np.ndarray):
+        raise TypeError("output buffer must be a numpy array or a torch tensor")
+    if not a.flags.c_contiguous or not a.flags.writeable:
+        raise ValueError("output buffer must be C-contiguous and writable")
+    if want_int16 and a.dtype != np.int16:
+        raise ValueError("output buffer must be int16 (got %s)" % a.dtype)
+    return a.ctypes.data, a.nbytes
+
+
 def decode_streams_into(datas, out, mode=MODE_EXACT, n_threads=0, n_groups=0, device=0):
     """Pipelined bitstreams-in, PCM-out (mp3g_decode_streams_into): groups of
     streams, each group's host scan overlapping the previous group's
-    transfers and kernels.  `out` is a writable int16 buffer (numpy array or
-    a pinned torch tensor) of at least 1152 * (total granules) samples; the
-    layout comes from a header-only pre-pass (streams[k].first_granule).
-    Returns (n_granules, streams, end_status)."""
+    transfers and kernels.  `out` is a writable, C-contiguous int16 host
+    buffer (numpy array or a pinned CPU torch tensor) of at least
+    1152 * (total granules) samples; the layout comes from a header-only
+    pre-pass (streams[k].first_granule).  Returns (n_granules, streams, end_status)."""
     bufs, ptrs, lens = _stream_args(datas)
     streams = np.zeros(len(datas), STREAM_DTYPE)
     status = np.zeros(max(1, len(datas)), np.int32)
     n = C.c_uint64()
-    if hasattr(out, "data_ptr"):
-        ptr, cap = out.data_ptr(), out.numel() // 1152
-    else:
-        ptr, cap = out.ctypes.data, out.size // 1152
+    ptr, nbytes = _host_buffer(out, want_int16=True)
+    cap = nbytes // MP3G_PCM_BYTES_PER_GRANULE
     _check(lib().mp3g_decode_streams_into(device, len(datas), ptrs, lens, n_threads, mode, n_groups,
                                           C.c_void_p(ptr), cap, C.byref(n), _ptr(streams), _ptr(status)))
     return n.value, streams, status[:len(datas)]
@@ -415,12 +439,9 @@ class Decoder:
         return st, out[:k.value].tobytes()
 
     def read_full(self, out):
-        """io.ReadFull into a writable buffer (numpy uint8/int16 array or a
-        pinned torch tensor): (status, bytes delivered)."""
-        if hasattr(out, "data_ptr"):
-            ptr, cap = out.data_ptr(), out.numel() * out.element_size()
-        else:
-            ptr, cap = out.ctypes.data, out.nbytes
+        """io.ReadFull into a writable, C-contiguous host buffer (numpy array
+        or CPU torch tensor of any dtype; filled as bytes): (status, bytes delivered)."""
+        ptr, cap = _host_buffer(out, want_int16=False)
         k = C.c_size_t()
         st = lib().mp3g_decoder_read_full(self._h, C.c_void_p(ptr), cap, C.byref(k))
         return st, k.value

@@ -30,7 +30,10 @@
 extern "C" {
 #endif
 
-#define MP3G_ABI_VERSION 1
+/* 2: mp3g_lame_toc_offset returns a status and writes the offset through an
+ *    out-parameter (version 1 returned the offset); the fast-mode hot-granule
+ *    fallback (no signature change). */
+#define MP3G_ABI_VERSION 2
 
 /* ---- status codes ------------------------------------------------------ */
 typedef enum mp3g_status {
@@ -141,11 +144,13 @@ int mp3g_validate(const mp3g_granule* granules, const int16_t* coeffs,
 
 /* ---- plans: device-resident work decomposition ---------------------------
  * A plan splits every stream into chunks processed by independent waves /
- * workgroups.  granules_per_chunk: k > 0 = chunks of k granules;
+ * workgroups.  granules_per_chunk: 0 < k < 2^31 = every stream cut into
+ * ceil(n / k) chunks of equal length +-1 (so at most k granules each);
  * 0 = automatic (a length from the launch-cost model, then the chunk count
  * rounded to whole rounds of resident chunks and every stream cut into
  * chunks of equal length +-1); MP3G_PLAN_CHUNKS(c) = about c chunks in total,
- * spread over the streams by length, equal lengths +-1.  A chunk that does
+ * spread over the streams by length, equal lengths +-1 (c < 2^31).  Every
+ * chunk holds < 2^32 granules (MP3G_ERR_UNSUPPORTED otherwise).  A chunk that does
  * not start a stream re-derives its entry state from the two preceding
  * granules (bit-identical to serial decode; DESIGN.md "halo").  The plan lives
  * on `device` and can be executed many times (graph-capturable). */

@@ -75,7 +75,7 @@ def test_struct_layouts_match_c(tmp_path):
 
 def test_status_strings_and_version():
     L = mp3g.lib()
-    assert L.mp3g_abi_version() == 1
+    assert L.mp3g_abi_version() == 2
     for s in range(9):
         assert L.mp3g_status_string(s) and L.mp3g_status_string(s) != b"unknown status"
 
@@ -157,3 +157,28 @@ def test_decode_streams_into_capacity_check_needs_no_device(sample_files):
                                               status.ctypes.data_as(C.c_void_p))
     assert rc == 1  # MP3G_ERR_INVALID_ARGUMENT
     assert n.value == 385 * 2 + 2872  # every frame of both streams: MPEG-1 two granules, MPEG-2 one
+
+
+def test_host_output_buffers_are_checked():
+    """decode_streams_into / Decoder.read_full write host memory through a raw
+    pointer: the Python layer refuses buffers whose size it would misjudge
+    (uint8 capacity read as int16, non-contiguous views, device
+    tensors) before anything reaches the library."""
+    import torch
+    import mp3g
+    with pytest.raises(ValueError):
+        mp3g.decode_streams_into([b"\xff\xfb"], np.zeros(4 * 1152, np.uint8))
+    with pytest.raises(ValueError):
+        mp3g.decode_streams_into([b"\xff\xfb"], np.zeros((2, 1152 * 2), np.int16)[:, ::2])
+    with pytest.raises(ValueError):
+        mp3g.decode_streams_into([b"\xff\xfb"], torch.zeros(1152, dtype=torch.int32))
+    with pytest.raises(TypeError):
+        mp3g.decode_streams_into([b"\xff\xfb"], bytearray(2304))
+    ro = np.zeros(1152, np.int16)
+    ro.flags.writeable = False
+    with pytest.raises(ValueError):
+        mp3g.decode_streams_into([b"\xff\xfb"], ro)
+    ptr, nb = mp3g._host_buffer(np.zeros((3, 1152), np.int16), want_int16=True)
+    assert nb == 3 * 2304
+    ptr, nb = mp3g._host_buffer(torch.zeros(100, dtype=torch.uint8), want_int16=False)
+    assert nb == 100

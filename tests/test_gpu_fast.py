@@ -211,3 +211,23 @@ def test_fast_all_hot_is_reference_order(gpu):
     pcm, _ = fast_plan(gpu, g, c, s)
     dmax, frac = assert_close(pcm, want, "all hot")
     assert frac < 1e-4, frac
+
+
+def test_fast_sparse_linbits_spikes(gpu):
+    """A few linbits-size lines per granule-channel (|x| = 3000 .. 8206) at
+    gains that put them far above kHotS: sparse, so the per-slot sums keep
+    them on the fast transforms (within +-1 LSB, tools/fast_tolerance.py)."""
+    rng = np.random.default_rng(21)
+    g, c, s = synth.synth_batch(3, 40, seed=57)
+    for gi in range(len(g)):
+        for ch in range(2):
+            pos = rng.choice(np.arange(int(g["ch"]["count1"][gi, ch])) if g["ch"]["count1"][gi, ch] > 3
+                             else np.arange(3), size=3, replace=False)
+            c[gi, ch, pos] = rng.choice([-8206, -3000, 3000, 8206], size=3)
+            g["ch"]["count1"][gi, ch] = max(int(g["ch"]["count1"][gi, ch]), int(pos.max()) + 1)
+    g["ch"]["global_gain"] = 150
+    want, _ = oracle.dsp_streams(g, c, s)
+    lines = oracle.hybrid_streams(g, c, s)
+    assert np.abs(lines).max() > 8.0
+    pcm, _ = fast_plan(gpu, g, c, s)
+    assert_close(pcm, want, "sparse linbits spikes")

@@ -188,3 +188,20 @@ def test_synth_empty_plan_and_errors(gpu):
     with pytest.raises(Exception):
         exact.synth_execute(x, x, x)  # standalone synthesis runs on fast-mode plans only
     exact.close()
+
+
+def test_synth_sparse_spikes(gpu):
+    """Lines far above kHotS but sparse (a few per granule-channel, as linbits
+    values are): the per-slot sums stay under kHotL1 = 64, so these granules
+    stay on the fast transforms -- measured within +-1 LSB there."""
+    rng = np.random.default_rng(12)
+    g, c, s = synth.synth_batch(4, 60, seed=93)
+    lines = oracle.hybrid_streams(g, c, s)
+    n = len(g)
+    for gi in range(n):
+        for ch in range(2):
+            pos = rng.choice(576, size=3, replace=False)
+            lines[gi, ch, pos] = rng.choice([-40.0, -20.0, 20.0, 40.0], size=3)
+    want, _ = oracle.synth_streams(g, lines, s)
+    got, _ = run_synth(gpu, g, lines, s)
+    assert_close(got, want, "sparse spikes")

@@ -70,8 +70,11 @@ def main():
             res["synth"].append(r)
             print("synth", r, flush=True)
     # fused kernel: long blocks, no scale factors, magnitude 2^((gg-210)/4) * |x|^(4/3)
-    for kind in ("rand15", "alt15", "altsb15", "rand1"):
-        for gg in (150, 160, 170, 180, 186, 190, 194, 198, 202, 210, 230, 255):
+    for kind in ("rand15", "alt15", "altsb15", "rand1", "spike", "spike+rand"):
+        ggs = (150, 160, 170, 180, 186, 190, 194, 198, 202, 210, 230, 255)
+        if kind.startswith("spike"):  # a few linbits-size lines: S ~ |x| ~ 8206^(4/3) 2^((gg-210)/4)
+            ggs = (120, 130, 136, 140, 144, 146, 148, 150, 152, 154, 156, 160)
+        for gg in ggs:
             g2, c2, s2 = synth.synth_batch(2, args.granules // 4, seed=9, p_is=0.0, p_event=0.0)
             n = len(g2)
             for ch in range(2):
@@ -87,6 +90,12 @@ def main():
                 c2[:] = rng.integers(-1, 2, size=(n, 2, 576))
             elif kind == "alt15":
                 c2[:] = np.where(i % 2 == 0, 15, -15)
+            elif kind.startswith("spike"):
+                c2[:] = rng.integers(-2, 3, size=(n, 2, 576)) if kind == "spike+rand" else 0
+                for gi in range(n):
+                    for ch in range(2):
+                        pos = rng.choice(576, size=3, replace=False)
+                        c2[gi, ch, pos] = rng.choice([-8206, -5000, 3000, 8206], size=3)
             else:
                 c2[:] = np.where((i // 18) % 2 == 0, 15, -15)
             c2 = c2.astype(np.int16)
@@ -94,7 +103,8 @@ def main():
             got, _ = run_plan(mp3g, g2, c2, s2, mode=mp3g.MODE_FAST)
             m, f = diff(got, want)
             lines = oracle.hybrid_streams(g2, c2, s2)
-            r = dict(kind=kind, gg=gg, max_abs_x=float(15 ** (4 / 3) * 2 ** ((gg - 210) / 4)),
+            xr = oracle.frontend_granules(g2, c2)
+            r = dict(kind=kind, gg=gg, max_abs_x=float(np.abs(xr).max()),
                      max_abs_S=float(np.abs(lines).max()), max_dpcm=m, frac=f,
                      clip=float((np.abs(want) == 32767).mean()))
             res["fused"].append(r)

@@ -21,6 +21,7 @@ run() {  # name timeout args...
   if [ $rc -ge 124 ]; then exit $rc; fi
   return 0
 }
+sha256sum go-mp3_amd/mp3g/libmp3g.so > $OUT/prof_${TAG}_lib.sha
 cfgs="c2 c3"; [ "$WHICH" != both ] && cfgs=$WHICH
 for cfg in $cfgs; do
   steps=20; [ $cfg = c3 ] && steps=5

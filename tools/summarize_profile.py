@@ -54,6 +54,11 @@ def main(src, tag, cfg, dst="profiles", bytes_per_launch=None, kernel=None, suff
     sq = counters(base + "_sq", kernel, grid)
     out = {"tag": tag, "config": cfg, "kernel": k["Name"].split("(")[0],
            "stats_calls": int(k["Calls"]), "stats_avg_ns": float(k["AverageNs"])}
+    # the library build the passes ran (tools/profile.sh records its sha256):
+    # bench.py flags traffic read from a profile of another build
+    shaf = os.path.join(src, f"prof_{tag}_lib.sha")
+    if os.path.exists(shaf):
+        out["lib_sha16"] = open(shaf).read().split()[0][:16]
     if durs:  # the full-grid launches only (kernel trace)
         avg_ns = sum(durs) / len(durs)
         out.update(grid=grid, calls=len(durs), avg_ns=avg_ns, min_ns=min(durs), max_ns=max(durs))
