@@ -13,7 +13,7 @@ import numpy as np
 
 from . import STREAM_DTYPE
 
-__all__ = ["shard_bounds", "shard_streams", "gather_pcm", "max_over_ranks"]
+__all__ = ["shard_bounds", "shard_streams", "shard_frames", "halo_start", "gather_pcm", "max_over_ranks"]
 
 
 def shard_bounds(n_items, world, rank):
@@ -45,6 +45,50 @@ def shard_streams(streams, world, rank):
     g_lo, g_hi = int(first[0]), int(ends.max())
     mine["first_granule"] = first - g_lo
     return mine, g_lo, g_hi
+
+
+def _stereo(headers):
+    return ((np.asarray(headers, dtype=np.uint32) >> 6) & 3) != 3  # frameheader.go:86-105 (mode 3 = mono)
+
+
+def halo_start(granules, g, stream_first=0):
+    """First granule a decode must start from, with zero state, so that its
+    state at granule `g` equals the serial decode's: the plans' replay rule
+    (granule_fast.hip prologue, DESIGN.md "halo").  store after g-1 is a
+    function of granule g-1 and vVec of granules g-2 and g-1
+    (frame.go:473-476, :637-652), so two granules back -- but a mono granule
+    leaves channel 1 untouched (Decode works on ch < nch, frame.go:125-133),
+    so channel 1's state comes from the two latest stereo granules before g.
+    (Conservative: always covers channel 1.)"""
+    g, s0 = int(g), int(stream_first)
+    if g <= s0:
+        return s0
+    start0 = max(s0, g - 2)
+    hdr = granules["header"] if granules.dtype.names else granules
+    st = _stereo(hdr[s0:g])  # index i <-> granule s0 + i
+    if len(st) >= 2 and st[-1] and st[-2]:
+        return start0
+    idx = np.nonzero(st)[0]
+    start1 = s0 + int(idx[-2]) if len(idx) >= 2 else s0
+    return min(start0, start1)
+
+
+def shard_frames(granules, world, rank, stream_first=0, n_granules=None):
+    """Contiguous granule ranges of ONE long stream ("for long
+    single streams, shard by contiguous frame ranges and duplicate 2 halo
+    granules"): rank r outputs granules [lo, hi) of the stream and decodes
+    [h, hi) from zero state, h = halo_start(lo), discarding the PCM of the
+    halo [h, lo).  Bit-identical to the serial decode in exact mode (and to a
+    one-GPU fast decode in fast mode).  A stream with state_in is not
+    supported (its halo would need the state at h).  Returns (h, lo, hi) in
+    global granule indices."""
+    n = len(granules) - int(stream_first) if n_granules is None else int(n_granules)
+    lo, hi = shard_bounds(n, world, rank)
+    lo += int(stream_first)
+    hi += int(stream_first)
+    if hi == lo:
+        return lo, lo, hi
+    return halo_start(granules, lo, stream_first), lo, hi
 
 
 def max_over_ranks(value, device=None):

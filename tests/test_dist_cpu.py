@@ -86,3 +86,38 @@ def test_gloo_shard_and_gather(world):
     assert status == "ok"
     assert t == 0.5 + (world - 1)  # max over ranks
     assert same, "gathered PCM differs from the full-batch decode"
+
+
+def test_halo_start_rule():
+    g, _, _ = synth.synth_batch(1, 20, seed=4)
+    assert mdist.halo_start(g, 0) == 0 and mdist.halo_start(g, 1) == 0
+    assert mdist.halo_start(g, 10) == 8  # two stereo granules back
+    mono = synth.header(synth.MODE_MONO)
+    g2 = g.copy()
+    g2["header"][[5, 6, 7, 8, 9]] = mono  # channel 1 last touched by granules 3 and 4
+    assert mdist.halo_start(g2, 10) == 3
+    assert mdist.halo_start(g2, 8) == 3
+    g2["header"][:10] = mono  # no stereo granule before 10: channel 1 is zero from the start
+    assert mdist.halo_start(g2, 10) == 0
+
+
+def test_shard_frames_partition_and_oracle_exact():
+    """Frame-range shards of one stream decoded from zero state (the oracle
+    as the per-rank decoder here; the GPU test runs the product): the halo
+    makes every shard's PCM bit-identical to the serial decode's."""
+    import oracle
+    parts = [synth.synth_stream(31, 30), synth.synth_stream(32, 9, mode=synth.MODE_MONO),
+             synth.synth_stream(33, 25)]
+    g = np.concatenate([p[0] for p in parts])
+    c = np.concatenate([p[1] for p in parts])
+    want, _ = oracle.dsp_streams(g, c, mp3g.streams_for([len(g)]))
+    for world in (1, 2, 3, 5, 8):
+        got = []
+        for r in range(world):
+            h, lo, hi = mdist.shard_frames(g, world, r)
+            assert h <= lo <= hi
+            if hi == lo:
+                continue
+            pcm, _ = oracle.dsp_streams(g[h:hi], c[h:hi], mp3g.streams_for([hi - h]))
+            got.append(pcm[lo - h:])
+        assert np.array_equal(np.concatenate(got), want), f"world {world}"
