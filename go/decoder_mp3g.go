@@ -1,0 +1,197 @@
+//go:build mp3g
+
+// Package mp3 -- the whole decoder behind the C-ABI (alternative to
+// frame_mp3g.go): mp3.NewDecoder / io.Reader / io.Seeker and the time API of
+// llehouerou/go-mp3 (decode.go:27-388) over mp3g_decoder_* (include/mp3g.h),
+// which scans on the host with read-ahead and decodes batches of frames on
+// the GPU (main data and DSP), carrying the DSP state between batches.
+// Also DecodeMany, the batch API for servers (mp3g_decode_streams).
+//
+// Written from include/mp3g.h (ABI version 2); tests/test_cgo_shim_cpu.py
+// checks every C identifier used here against the header.
+package mp3
+
+/*
+#cgo CFLAGS: -I${SRCDIR}/third_party/mp3g/include
+#cgo LDFLAGS: -L${SRCDIR}/third_party/mp3g/lib -lmp3g -Wl,-rpath,${SRCDIR}/third_party/mp3g/lib
+#include <stdlib.h>
+#include "mp3g.h"
+*/
+import "C"
+
+import (
+	"errors"
+	"fmt"
+	"io"
+	"time"
+	"unsafe"
+)
+
+// Mode: bit-exact PCM or within +-1 LSB of the reference (faster).
+var Mode C.uint32_t = C.MP3G_MODE_EXACT
+
+func statusError(st C.int) error {
+	switch st {
+	case C.MP3G_OK:
+		return nil
+	case C.MP3G_EOF:
+		return io.EOF
+	}
+	return fmt.Errorf("mp3: %s: %s", C.GoString(C.mp3g_status_string(st)), C.GoString(C.mp3g_last_error()))
+}
+
+// Decoder is a MP3-decoded stream (decode.go:34-43). Not safe for concurrent use.
+type Decoder struct{ d *C.mp3g_decoder }
+
+// NewDecoder decodes the given io.Reader (decode.go:361-388); the whole
+// stream is read up front and copied by the library (nothing Go-owned is
+// retained across calls).
+func NewDecoder(r io.Reader) (*Decoder, error) {
+	data, err := io.ReadAll(r)
+	if err != nil {
+		return nil, err
+	}
+	_, seekable := r.(io.Seeker)
+	var p *C.uint8_t
+	if len(data) > 0 {
+		p = (*C.uint8_t)(unsafe.Pointer(&data[0]))
+	}
+	s := C.int(0)
+	if seekable {
+		s = 1
+	}
+	var d *C.mp3g_decoder
+	if st := C.mp3g_decoder_new(p, C.size_t(len(data)), s, 0, Mode, &d); st != C.MP3G_OK {
+		return nil, statusError(st)
+	}
+	return &Decoder{d}, nil
+}
+
+// Close releases the decoder's host and device memory.
+func (d *Decoder) Close() error {
+	if d.d != nil {
+		C.mp3g_decoder_free(d.d)
+		d.d = nil
+	}
+	return nil
+}
+
+// Read is io.Reader's Read (decode.go:70-80): at most the rest of one frame.
+func (d *Decoder) Read(buf []byte) (int, error) {
+	if len(buf) == 0 {
+		return 0, nil
+	}
+	var n C.size_t
+	st := C.mp3g_decoder_read(d.d, (*C.uint8_t)(unsafe.Pointer(&buf[0])), C.size_t(len(buf)), &n)
+	if st != C.MP3G_OK {
+		return int(n), statusError(st)
+	}
+	return int(n), nil
+}
+
+// ReadFull is io.ReadFull(d, buf) in one cgo call.
+func (d *Decoder) ReadFull(buf []byte) (int, error) {
+	if len(buf) == 0 {
+		return 0, nil
+	}
+	var n C.size_t
+	st := C.mp3g_decoder_read_full(d.d, (*C.uint8_t)(unsafe.Pointer(&buf[0])), C.size_t(len(buf)), &n)
+	switch {
+	case st == C.MP3G_OK:
+		return int(n), nil
+	case st == C.MP3G_EOF && n == 0:
+		return 0, io.EOF
+	case st == C.MP3G_EOF:
+		return int(n), io.ErrUnexpectedEOF
+	}
+	return int(n), statusError(st)
+}
+
+// Seek is io.Seeker's Seek (decode.go:89-145), with the reference's warm-up.
+func (d *Decoder) Seek(offset int64, whence int) (int64, error) {
+	var np C.int64_t
+	if st := C.mp3g_decoder_seek(d.d, C.int64_t(offset), C.int(whence), &np); st != C.MP3G_OK {
+		return 0, statusError(st)
+	}
+	return int64(np), nil
+}
+
+func (d *Decoder) info() (sr int, length, bpf, pos int64) {
+	var s C.int
+	var l, b, p C.int64_t
+	C.mp3g_decoder_info(d.d, &s, &l, &b, &p)
+	return int(s), int64(l), int64(b), int64(p)
+}
+
+// SampleRate (decode.go:147-150).
+func (d *Decoder) SampleRate() int { sr, _, _, _ := d.info(); return sr }
+
+// Length in bytes, -1 when the reader is not an io.Seeker (decode.go:218-224).
+func (d *Decoder) Length() int64 { _, l, _, _ := d.info(); return l }
+
+// BytesPerFrame (decode.go:226-230).
+func (d *Decoder) BytesPerFrame() int64 { _, _, b, _ := d.info(); return b }
+
+// Duration, Position, Remaining, Progress, SamplePosition, SampleCount,
+// SeekToSample, Skip, SeekToTime: the time API (decode.go:232-354).
+func (d *Decoder) Duration() time.Duration { return time.Duration(C.mp3g_decoder_duration_ns(d.d)) }
+func (d *Decoder) Position() time.Duration { return time.Duration(C.mp3g_decoder_position_ns(d.d)) }
+func (d *Decoder) Remaining() time.Duration {
+	return time.Duration(C.mp3g_decoder_remaining_ns(d.d))
+}
+func (d *Decoder) Progress() float64     { return float64(C.mp3g_decoder_progress(d.d)) }
+func (d *Decoder) SamplePosition() int64 { return int64(C.mp3g_decoder_sample_position(d.d)) }
+func (d *Decoder) SampleCount() int64    { return int64(C.mp3g_decoder_sample_count(d.d)) }
+func (d *Decoder) SeekToSample(s int64) error {
+	return statusError(C.mp3g_decoder_seek_to_sample(d.d, C.int64_t(s)))
+}
+func (d *Decoder) SeekToTime(t time.Duration) error {
+	return statusError(C.mp3g_decoder_seek_to_time_ns(d.d, C.int64_t(t)))
+}
+func (d *Decoder) Skip(dt time.Duration) error {
+	return statusError(C.mp3g_decoder_skip_ns(d.d, C.int64_t(dt)))
+}
+
+// DecodeMany decodes complete MP3 files on the GPU, the main data included:
+// pcm[i] is what io.ReadAll(NewDecoder(file i)) returns, errs[i] the error
+// that ended file i after its PCM (nil for io.EOF).
+func DecodeMany(files [][]byte) ([][]byte, []error) {
+	n := len(files)
+	out, errs := make([][]byte, n), make([]error, n)
+	if n == 0 {
+		return out, errs
+	}
+	datas := (*[1 << 30]*C.uint8_t)(C.malloc(C.size_t(n) * C.size_t(unsafe.Sizeof(uintptr(0)))))[:n:n]
+	defer C.free(unsafe.Pointer(&datas[0]))
+	lens := make([]C.size_t, n)
+	for i, f := range files { // C memory: the call reads it, nothing is retained
+		datas[i] = (*C.uint8_t)(C.CBytes(f))
+		lens[i] = C.size_t(len(f))
+		defer C.free(unsafe.Pointer(datas[i]))
+	}
+	streams := make([]C.mp3g_stream, n)
+	status := make([]C.int, n)
+	var pcm *C.int16_t
+	var ng C.uint64_t
+	st := C.mp3g_decode_streams(0, C.uint32_t(n), &datas[0], &lens[0], 0, Mode, &pcm, &ng,
+		&streams[0], &status[0])
+	if st != C.MP3G_OK {
+		e := statusError(st)
+		for i := range errs {
+			errs[i] = e
+		}
+		return out, errs
+	}
+	defer C.mp3g_free(unsafe.Pointer(pcm))
+	all := unsafe.Slice((*byte)(unsafe.Pointer(pcm)), int(ng)*C.MP3G_PCM_BYTES_PER_GRANULE)
+	for i := range files {
+		s := streams[i]
+		lo := int(s.first_granule) * C.MP3G_PCM_BYTES_PER_GRANULE
+		hi := lo + int(s.n_granules)*C.MP3G_PCM_BYTES_PER_GRANULE
+		out[i] = append([]byte(nil), all[lo:hi]...)
+		if e := statusError(status[i]); !errors.Is(e, io.EOF) {
+			errs[i] = e
+		}
+	}
+	return out, errs
+}

@@ -1,0 +1,116 @@
+"""The committed cgo shim (go/*.go, build tag mp3g) against include/mp3g.h.
+
+There is no Go toolchain in this image, so the shim cannot be compiled here;
+this test does the mechanical part of that check: every C identifier the Go
+files use exists in the header (functions, types, constants), every C call
+passes as many arguments as the prototype declares, and every struct field
+the shim writes is a field of that struct.  Reference seams: frame.go:121
+(Frame.Decode) and decode.go:65 (its only call site).
+"""
+import os
+import re
+
+from conftest import REPO
+
+HEADER = open(os.path.join(REPO, "include", "mp3g.h")).read()
+GO = {f: open(os.path.join(REPO, "go", f)).read() for f in sorted(os.listdir(os.path.join(REPO, "go")))
+      if f.endswith(".go")}
+CGO_BUILTINS = {"malloc", "free", "CBytes", "GoString", "CString", "GoBytes"}
+C_SCALARS = {"int", "uint", "size_t", "int16_t", "uint8_t", "uint16_t", "uint32_t", "uint64_t", "int64_t",
+             "double", "float", "char"}
+
+
+def _strip_comments(src):
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return re.sub(r"//[^\n]*", "", src)
+
+
+def prototypes():
+    """name -> parameter count of every function the header declares."""
+    out = {}
+    for m in re.finditer(r"\b(?:int|void|double|int64_t|const char\*)\s+\**(mp3g_\w+)\(([^;{]*?)\);",
+                         _strip_comments(HEADER), flags=re.S):
+        params = m.group(2).strip()
+        out[m.group(1)] = 0 if params in ("", "void") else params.count(",") + 1
+    return out
+
+
+def struct_fields(name):
+    m = re.search(r"typedef struct %s \{(.*?)\} %s;" % (name, name), _strip_comments(HEADER), flags=re.S)
+    assert m, name
+    return set(re.findall(r"(\w+)\s*(?:\[[^\]]*\])*\s*;", m.group(1)))
+
+
+def call_args(src, start):
+    """Number of top-level arguments of the call whose '(' is at src[start]."""
+    depth, n, seen = 0, 0, False
+    for ch in src[start:]:
+        if ch == "(":
+            depth += 1
+            if depth == 1:
+                continue
+        elif ch == ")":
+            depth -= 1
+            if depth == 0:
+                return n + 1 if seen else 0
+        elif ch == "," and depth == 1:
+            n += 1
+        if depth >= 1 and not ch.isspace():
+            seen = True
+    raise AssertionError("unbalanced call")
+
+
+def test_go_shim_files_present():
+    assert "frame_mp3g.go" in GO and "decoder_mp3g.go" in GO
+    for f, src in GO.items():
+        assert src.startswith("//go:build mp3g"), f
+        assert 'import "C"' in src and '#include "mp3g.h"' in src, f
+
+
+def test_c_identifiers_and_call_arity_match_the_header():
+    protos = prototypes()
+    hdr = _strip_comments(HEADER)
+    for f, src in GO.items():
+        code = _strip_comments(src.split('import "C"', 1)[1])
+        for m in re.finditer(r"\bC\.(\w+)", code):
+            name = m.group(1)
+            after = code[m.end():m.end() + 1]
+            if name in CGO_BUILTINS or name in C_SCALARS:
+                continue
+            if name.startswith("mp3g_") and after == "(" and name in protos:
+                got = call_args(code, m.end())
+                assert got == protos[name], f"{f}: C.{name} called with {got} args, header declares {protos[name]}"
+            elif name.startswith("mp3g_"):
+                assert re.search(r"\b%s\b" % name, hdr), f"{f}: C.{name} not in mp3g.h"
+                if after == "(":  # a conversion to a header type, e.g. (*C.mp3g_granule)(...)
+                    assert re.search(r"typedef struct %s\b" % name, hdr), f"{f}: C.{name}(...) unknown"
+            elif name.startswith("MP3G_"):
+                assert re.search(r"(#define\s+%s\b|\b%s\s*=)" % (name, name), hdr), f"{f}: C.{name} not in mp3g.h"
+            else:
+                raise AssertionError(f"{f}: unexpected C.{name}")
+
+
+def test_struct_fields_written_by_the_shim_exist():
+    ch = struct_fields("mp3g_channel")
+    gr = struct_fields("mp3g_granule")
+    st = struct_fields("mp3g_stream")
+    src = _strip_comments(GO["frame_mp3g.go"])
+    for fld in re.findall(r"\bc\.(\w+)", src):
+        assert fld in ch, f"mp3g_channel has no field {fld}"
+    for fld in re.findall(r"\bg\.(\w+)\s*=", src):
+        assert fld in gr, f"mp3g_granule has no field {fld}"
+    for go in GO.values():
+        for lit in re.findall(r"C\.mp3g_stream\{([^}]*)\}", go):
+            for fld in re.findall(r"(\w+)\s*:", lit):
+                assert fld in st, f"mp3g_stream has no field {fld}"
+        for fld in re.findall(r"\bs\.(first_granule|n_granules|flags)\b", go):
+            assert fld in st
+    # the fields Decode reads are all copied
+    for fld in ("count1", "global_gain", "scalefac_scale", "preflag", "win_switch_flag", "block_type",
+                "mixed_block_flag", "subblock_gain", "scalefac_l", "scalefac_s"):
+        assert re.search(r"\bc\.%s\b" % fld, src), f"frame_mp3g.go does not copy {fld}"
+
+
+def test_abi_version_matches():
+    v = int(re.search(r"#define MP3G_ABI_VERSION (\d+)", HEADER).group(1))
+    assert f"const ABIVersion = {v}" in GO["frame_mp3g.go"]
