@@ -190,19 +190,26 @@ def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle, pip
     mp3g.lib().mp3g_release_cached_buffers()
     # the io.Reader drop-in (mp3.NewDecoder + Read, decode.go:70-80, 361-388)
     # on the first stream: read-ahead batches (host scan, then the Huffman and
-    # DSP kernels with the state carried between batches), 1 MiB reads
+    # DSP kernels with the state carried between batches), 1 MiB reads.  Twice:
+    # the first decoder of the process pins its PCM buffers, which the library
+    # pools for later decoders (a server decodes one stream after another);
+    # the time of the second
     rbuf = np.empty(1 << 20, np.uint8)
-    t = time.perf_counter()
+    dec_data = datas[0] if cfg == "c2" else synth.encode_stream(seed0, 10000)  # the c2 stream
+    dec_times = []
     got_bytes, st_r = 0, None
-    if pipelined:
-        dec = mp3g.Decoder(datas[0], mode=mode, device=idx)
+    for _ in range(2 if pipelined else 0):
+        t = time.perf_counter()
+        got_bytes, st_r = 0, None
+        dec = mp3g.Decoder(dec_data, mode=mode, device=idx)
         while True:
             st_r, k = dec.read_full(rbuf)  # io.ReadFull: Read until 1 MiB (Read gives <= 1 frame)
             got_bytes += k
             if st_r != 0:
                 break
         dec.close()
-    dec_s = time.perf_counter() - t
+        dec_times.append(time.perf_counter() - t)
+    dec_s = dec_times[-1] if dec_times else float("nan")
     dec_frames = got_bytes // 4608
     frames = n // 2
     md = int(s["main_data"].nbytes)
@@ -230,7 +237,10 @@ def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle, pip
                           "pcm_d2h_bytes": int(n * 2304)},
            "decoder_api": None if not pipelined else {
                            "frames_per_s": round(dec_frames / dec_s, 1), "frames": int(dec_frames),
-                           "api": "mp3g_decoder_new + mp3g_decoder_read_full (io.ReadFull of 1 MiB), one stream",
+                           "api": "mp3g_decoder_new + mp3g_decoder_read_full (io.ReadFull of 1 MiB), one stream "
+                                  "(the c2 bitstream: 10,000 frames)",
+                           "first_decoder_s": round(dec_times[0], 4),
+                           "note": "the second decoder of the process (pinned / device buffers pooled by the library)",
                            "read_status": int(st_r)}}
     if check_oracle:
         sys.path.insert(0, os.path.join(REPO, "oracle"))

@@ -32,6 +32,12 @@ namespace mp3g {
 namespace v3 {
 
 constexpr int kSynthWaves = 8;
+// MP3G_SYNTH_ABL (diagnostic builds only, wrong PCM): leave out LDS access
+// groups to read SQ_LDS_BANK_CONFLICT per group (tools/gpu_synthlds.sh):
+// 1 staging writes, 2 matrixing, 4 window reads, 8 history shift
+#ifndef MP3G_SYNTH_ABL
+#define MP3G_SYNTH_ABL 0
+#endif
 
 struct __align__(16) SynthWaveSmem {
   float ring[2][32][kSlots];
@@ -211,7 +217,7 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
 #if MP3G_HOT_CHECK
     const bool hot1 = __builtin_amdgcn_ballot_w64(max_abs_pairs(A) > kHotS) != 0;
 #endif
-    synth_stage(s, A, nch);
+    if (!(MP3G_SYNTH_ABL & 1)) synth_stage(s, A, nch);
     // the next granule in flight during the matrixing and window
     load(g + 1, A);
     wave_sync();
@@ -223,7 +229,7 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
     // ---- matrixing (frame.go:642-648): lane (ch, slot) turns its S row into X ----
     {
       const int slot = lane & 31;
-      if (ch < nch && slot < 18) {
+      if (!(MP3G_SYNTH_ABL & 2) && ch < nch && slot < 18) {
         float* colu = &s.ring[ch][0][kHist + slot];
         dct32::f2 sp[16];
 #pragma unroll
@@ -237,7 +243,7 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
     wave_sync();
     // ---- 16-tap window -> s16 PCM (frame.go:649-678); the stores are issued
     //      for replayed granules too, through a resource with no records ----
-    if (out) {
+    if (out && !(MP3G_SYNTH_ABL & 4)) {
       const f2* RA = reinterpret_cast<const f2*>(&s.ring[ch][pa][0]);
       const float* RB = &s.ring[ch][pb][0];
       f2 acc2[9];
@@ -261,7 +267,7 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
     store_pcm(pcm, g, out, pk, hi, k);
     wave_sync();
     // ---- history shift of the channels this granule touched ----
-    if (ch < nch) {
+    if (!(MP3G_SYNTH_ABL & 8) && ch < nch) {
       f2* col = reinterpret_cast<f2*>(&s.ring[ch][k][0]);
 #pragma unroll
       for (int q = 0; q < 8; q++) col[q] = col[9 + q];

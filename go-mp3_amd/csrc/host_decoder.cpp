@@ -16,7 +16,10 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdlib>
+#include <chrono>
+#include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <thread>
 #include <vector>
@@ -62,8 +65,137 @@ St parse_all(const uint8_t* data, size_t len, std::vector<mp3g_granule>* g, std:
 
 }  // namespace
 
-// PCM read-ahead bytes in page-locked memory: the batch's PCM is copied from
-// the device straight into it (no pageable bounce, no second host copy).
+// Page-locked blocks for the decoders' PCM read-ahead, pooled per process:
+// pinning is the expensive part of a decoder's life (hipHostMalloc of the
+// 37 MB a full batch needs takes milliseconds), so a freed decoder's blocks
+// serve the next one.  mp3g_release_cached_buffers empties the pool.
+namespace {
+struct PinnedBlock {
+  uint8_t* p;
+  size_t cap;
+  bool pinned;
+};
+std::mutex g_pin_mu;
+std::vector<PinnedBlock> g_pin_pool;
+constexpr size_t kPinPoolMax = 8;
+
+PinnedBlock pin_take(size_t need) {
+  {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    // the smallest pooled block that fits
+    size_t best = g_pin_pool.size();
+    for (size_t i = 0; i < g_pin_pool.size(); i++)
+      if (g_pin_pool[i].cap >= need && (best == g_pin_pool.size() || g_pin_pool[i].cap < g_pin_pool[best].cap)) best = i;
+    if (best < g_pin_pool.size()) {
+      const PinnedBlock b = g_pin_pool[best];
+      g_pin_pool.erase(g_pin_pool.begin() + best);
+      return b;
+    }
+  }
+  void* q = nullptr;
+  const bool pin = hipHostMalloc(&q, need, hipHostMallocDefault) == hipSuccess;
+  if (!pin) q = std::malloc(need);
+  return {static_cast<uint8_t*>(q), q ? need : 0, pin};
+}
+
+void pin_free(const PinnedBlock& b) {
+  if (b.pinned) (void)hipHostFree(b.p);
+  else std::free(b.p);
+}
+
+void pin_give(const PinnedBlock& b) {
+  if (!b.p) return;
+  PinnedBlock drop{nullptr, 0, false};
+  {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    g_pin_pool.push_back(b);
+    if (g_pin_pool.size() > kPinPoolMax) {  // keep the largest blocks
+      size_t small = 0;
+      for (size_t i = 1; i < g_pin_pool.size(); i++)
+        if (g_pin_pool[i].cap < g_pin_pool[small].cap) small = i;
+      drop = g_pin_pool[small];
+      g_pin_pool.erase(g_pin_pool.begin() + small);
+    }
+  }
+  if (drop.p) pin_free(drop);
+}
+// Device blocks of the decoders (granules, coefficients, PCM, jobs of a
+// batch in one block; the main data in another), pooled per process and
+// device like the pinned blocks: a decoder's first batches would otherwise
+// pay a hipFree + hipMalloc every time the read-ahead doubles.
+struct DevBlock {
+  void* p;
+  size_t cap;
+  int device;
+};
+std::vector<DevBlock> g_dev_pool;  // guarded by g_pin_mu
+
+DevBlock dev_take(int device, size_t need) {
+  {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    size_t best = g_dev_pool.size();
+    for (size_t i = 0; i < g_dev_pool.size(); i++)
+      if (g_dev_pool[i].device == device && g_dev_pool[i].cap >= need &&
+          (best == g_dev_pool.size() || g_dev_pool[i].cap < g_dev_pool[best].cap))
+        best = i;
+    if (best < g_dev_pool.size()) {
+      const DevBlock b = g_dev_pool[best];
+      g_dev_pool.erase(g_dev_pool.begin() + best);
+      return b;
+    }
+  }
+  void* q = nullptr;
+  if (hipMalloc(&q, need) != hipSuccess) return {nullptr, 0, device};
+  return {q, need, device};
+}
+
+void dev_give(const DevBlock& b) {
+  if (!b.p) return;
+  DevBlock drop{nullptr, 0, 0};
+  {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    g_dev_pool.push_back(b);
+    if (g_dev_pool.size() > kPinPoolMax) {
+      size_t small = 0;
+      for (size_t i = 1; i < g_dev_pool.size(); i++)
+        if (g_dev_pool[i].cap < g_dev_pool[small].cap) small = i;
+      drop = g_dev_pool[small];
+      g_dev_pool.erase(g_dev_pool.begin() + small);
+    }
+  }
+  if (drop.p) {
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(drop.device);
+    (void)hipFree(drop.p);
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+}
+}  // namespace
+
+void release_pinned_pool() {
+  std::vector<PinnedBlock> v;
+  {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    v.swap(g_pin_pool);
+  }
+  for (const PinnedBlock& b : v) pin_free(b);
+  std::vector<DevBlock> dv;
+  {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    dv.swap(g_dev_pool);
+  }
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  for (const DevBlock& b : dv) {
+    (void)hipSetDevice(b.device);
+    (void)hipFree(b.p);
+  }
+  if (prev >= 0) (void)hipSetDevice(prev);
+}
+
+// PCM read-ahead bytes in page-locked memory (from the pool): the batch's
+// PCM is copied from the device straight into it (no pageable bounce).
 struct PinnedBytes {
   uint8_t* p = nullptr;
   size_t n = 0, cap = 0;
@@ -73,10 +205,7 @@ struct PinnedBytes {
   PinnedBytes& operator=(const PinnedBytes&) = delete;
   ~PinnedBytes() { release(); }
   void release() {
-    if (p) {
-      if (pinned) (void)hipHostFree(p);
-      else std::free(p);
-    }
+    if (p) pin_give({p, cap, pinned});
     p = nullptr;
     n = cap = 0;
   }
@@ -86,18 +215,15 @@ struct PinnedBytes {
   // room for `more` bytes past n (contents kept)
   bool reserve_more(size_t more) {
     if (n + more <= cap) return true;
-    const size_t c = std::max(n + more, 2 * cap);
-    void* q = nullptr;
-    bool pin = hipHostMalloc(&q, c, hipHostMallocDefault) == hipSuccess;
-    if (!pin) q = std::malloc(c);
-    if (!q) return false;
-    if (n) std::memcpy(q, p, n);
+    const PinnedBlock b = pin_take(std::max(n + more, 2 * cap));
+    if (!b.p) return false;
+    if (n) std::memcpy(b.p, p, n);
     const size_t keep = n;
     release();
-    p = static_cast<uint8_t*>(q);
+    p = b.p;
     n = keep;
-    cap = c;
-    pinned = pin;
+    cap = b.cap;
+    pinned = b.pinned;
     return true;
   }
 };
@@ -149,6 +275,9 @@ struct mp3g_decoder {
   int64_t pos = 0;
   // PCM being served (one batch) and the PCM of the batch on the device
   PinnedBytes buf, ahead;
+  // the batch's inputs in page-locked memory, so that their H2D copies are
+  // asynchronous (reused: a submit follows the previous batch's completion)
+  PinnedBytes stage;
   size_t buf_off = 0;
   int pending = MP3G_OK;  // parse error to report once buf runs dry
   bool scan_fresh = true;  // the next scanned batch starts from zero DSP state
@@ -168,10 +297,14 @@ struct mp3g_decoder {
   mp3g_hjob* d_jobs = nullptr;
   uint8_t* d_md = nullptr;
   size_t cap_granules = 0, cap_md = 0;
+  DevBlock blk{nullptr, 0, 0}, md_blk{nullptr, 0, 0};  // (pooled) device blocks behind the pointers above
   // the last plan (batches of the same length and state flags reuse it)
   mp3g_plan* plan = nullptr;
   uint64_t plan_n = 0;
   uint32_t plan_flags = 0;
+  // diagnostics (MP3G_DEC_STATS=1: printed to stderr when the decoder is freed)
+  double t_scan = 0, t_submit = 0, t_wait = 0, t_copy = 0, t_plan = 0, t_pin = 0, t_h2d = 0, t_exec = 0, t_d2h = 0;
+  long n_batches = 0;
   std::vector<size_t> frame_ends;         // end offset in buf of each buffered frame
   std::vector<int64_t> frame_src_ends;    // source position after each buffered frame
   // index into frame_ends of the frame the reference read last: Decoder.Read
@@ -180,6 +313,10 @@ struct mp3g_decoder {
   size_t next_end = 0;
 
   ~mp3g_decoder() {
+    if (std::getenv("MP3G_DEC_STATS"))
+      std::fprintf(stderr, "mp3g_decoder: %ld batches, scan %.2f ms, submit %.2f ms (plan %.2f, pin %.2f, h2d+huffman %.2f, "
+                   "dsp %.2f, d2h %.2f), wait %.2f ms, copy %.2f ms\n", n_batches, 1e3 * t_scan, 1e3 * t_submit, 1e3 * t_plan,
+                   1e3 * t_pin, 1e3 * t_h2d, 1e3 * t_exec, 1e3 * t_d2h, 1e3 * t_wait, 1e3 * t_copy);
     int prev = -1;
     (void)hipGetDevice(&prev);
     (void)hipSetDevice(device);
@@ -187,25 +324,38 @@ struct mp3g_decoder {
     if (plan) mp3g_plan_destroy(plan);
     buf.release();
     ahead.release();
-    for (void* p : {(void*)d_gran, (void*)d_coef, (void*)d_pcm, (void*)d_state, (void*)d_jobs, (void*)d_md})
-      if (p) (void)hipFree(p);
+    if (d_state) (void)hipFree(d_state);
+    dev_give(blk);
+    dev_give(md_blk);
     if (stream) (void)hipStreamDestroy(stream);
     if (prev >= 0) (void)hipSetDevice(prev);
   }
 
   int ensure_capacity(size_t n) {
     if (n <= cap_granules) return MP3G_OK;
-    size_t cap = std::max<size_t>(n, cap_granules * 2);
-    for (void** p : {(void**)&d_gran, (void**)&d_coef, (void**)&d_pcm, (void**)&d_jobs})
-      if (*p) { (void)hipFree(*p); *p = nullptr; }
-    if (hipMalloc(&d_gran, cap * sizeof(mp3g_granule)) != hipSuccess ||
-        hipMalloc(&d_coef, cap * MP3G_COEF_PER_GRANULE * sizeof(int16_t)) != hipSuccess ||
-        hipMalloc(&d_pcm, cap * MP3G_PCM_BYTES_PER_GRANULE) != hipSuccess ||
-        hipMalloc(&d_jobs, 2 * cap * sizeof(mp3g_hjob)) != hipSuccess) {
+    // at least 4,096 granules: the doubling read-ahead then reallocates twice
+    const size_t cap = std::max<size_t>({n, cap_granules * 2, 4096});
+    constexpr size_t kPerGranule =
+        sizeof(mp3g_granule) + MP3G_COEF_PER_GRANULE * sizeof(int16_t) + MP3G_PCM_BYTES_PER_GRANULE + 2 * sizeof(mp3g_hjob);
+    dev_give(blk);
+    blk = dev_take(device, cap * kPerGranule);
+    if (!blk.p) {
       cap_granules = 0;
+      d_gran = nullptr;
+      d_coef = d_pcm = nullptr;
+      d_jobs = nullptr;
       return abi_fail(MP3G_ERR_OUT_OF_MEMORY, "decoder device buffers");
     }
-    cap_granules = cap;
+    const size_t have = blk.cap / kPerGranule;  // a pooled block may be larger
+    uint8_t* q = static_cast<uint8_t*>(blk.p);
+    d_gran = reinterpret_cast<mp3g_granule*>(q);
+    q += have * sizeof(mp3g_granule);
+    d_coef = reinterpret_cast<int16_t*>(q);
+    q += have * MP3G_COEF_PER_GRANULE * sizeof(int16_t);
+    d_pcm = reinterpret_cast<int16_t*>(q);
+    q += have * MP3G_PCM_BYTES_PER_GRANULE;
+    d_jobs = reinterpret_cast<mp3g_hjob*>(q);
+    cap_granules = have;
     return MP3G_OK;
   }
 
@@ -215,6 +365,12 @@ struct mp3g_decoder {
   // the batch: b.err, the reservoir is dropped and the next batch starts from
   // zero DSP state (d.frame = nil after a failed frame.Read).
   void scan_batch(Batch& b, size_t max_frames) {
+    const auto t0 = std::chrono::steady_clock::now();
+    struct Acc {
+      double& t;
+      std::chrono::steady_clock::time_point t0;
+      ~Acc() { t += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); }
+    } acc{t_scan, t0};
     b.clear();
     b.fresh = scan_fresh;
     St st = St::kOk;
@@ -265,6 +421,12 @@ struct mp3g_decoder {
   // Enqueues batch b (n() > 0) on the decoder's stream: H2D, Huffman kernel,
   // DSP plan (state carried on the device), PCM D2H into `ahead`.
   int submit(const Batch& b) {
+    struct Acc {
+      double& t;
+      std::chrono::steady_clock::time_point t0;
+      ~Acc() { t += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); }
+    } acc{t_submit, std::chrono::steady_clock::now()};
+    n_batches++;
     const size_t n = b.n();
     int prev = -1;
     (void)hipGetDevice(&prev);
@@ -280,6 +442,12 @@ struct mp3g_decoder {
     int rc = ensure_capacity(n);
     if (rc) return rc;
     mp3g_stream s{0, (uint32_t)n, (b.fresh ? 0u : (uint32_t)MP3G_STREAM_STATE_IN) | MP3G_STREAM_STATE_OUT};
+    auto tp0 = std::chrono::steady_clock::now();
+    auto lap = [&](double& t) {
+      const auto now = std::chrono::steady_clock::now();
+      t += std::chrono::duration<double>(now - tp0).count();
+      tp0 = now;
+    };
     if (!plan || plan_n != n || plan_flags != s.flags) {
       if (plan) mp3g_plan_destroy(plan);
       plan = nullptr;
@@ -288,35 +456,52 @@ struct mp3g_decoder {
       plan_n = n;
       plan_flags = s.flags;
     }
+    lap(t_plan);
     const size_t pcm_bytes = n * MP3G_PCM_BYTES_PER_GRANULE;
     ahead.clear();
     if (!ahead.reserve_more(pcm_bytes)) return abi_fail(MP3G_ERR_OUT_OF_MEMORY, "decoder PCM buffer");
-    hipError_t e = hipMemcpyAsync(d_gran, b.gran.data(), n * sizeof(mp3g_granule), hipMemcpyHostToDevice, stream);
+    lap(t_pin);
+    // inputs into the pinned stage, then asynchronous H2D copies
+    const size_t b_gran = n * sizeof(mp3g_granule);
+    const size_t b_in = gpu_huffman() ? b.jobs.size() * sizeof(mp3g_hjob) + b.md.size()
+                                      : b.coef.size() * sizeof(int16_t);
+    stage.clear();
+    if (!stage.reserve_more(b_gran + b_in)) return abi_fail(MP3G_ERR_OUT_OF_MEMORY, "decoder staging buffer");
+    uint8_t* sg = stage.p;
+    std::memcpy(sg, b.gran.data(), b_gran);
+    hipError_t e = hipMemcpyAsync(d_gran, sg, b_gran, hipMemcpyHostToDevice, stream);
+    uint8_t* si = sg + b_gran;
     if (gpu_huffman()) {
       // main data + jobs up, then scale factors / Huffman codes on the device
       const size_t mdb = b.md.size() + 16;  // + padding for the 32-bit window loads
       if (e == hipSuccess && mdb > cap_md) {
-        if (d_md) (void)hipFree(d_md);
-        d_md = nullptr;
-        cap_md = std::max(mdb, 2 * cap_md);
-        e = hipMalloc(&d_md, cap_md);
-        if (e != hipSuccess) cap_md = 0;
+        dev_give(md_blk);
+        md_blk = dev_take(device, std::max<size_t>({mdb, 2 * cap_md, size_t(1) << 20}));
+        d_md = static_cast<uint8_t*>(md_blk.p);
+        cap_md = md_blk.cap;
+        if (!d_md) e = hipErrorOutOfMemory;
       }
+      const size_t b_jobs = b.jobs.size() * sizeof(mp3g_hjob);
+      std::memcpy(si, b.jobs.data(), b_jobs);
+      if (!b.md.empty()) std::memcpy(si + b_jobs, b.md.data(), b.md.size());
       if (e == hipSuccess && !b.md.empty())
-        e = hipMemcpyAsync(d_md, b.md.data(), b.md.size(), hipMemcpyHostToDevice, stream);
-      if (e == hipSuccess)
-        e = hipMemcpyAsync(d_jobs, b.jobs.data(), b.jobs.size() * sizeof(mp3g_hjob), hipMemcpyHostToDevice, stream);
+        e = hipMemcpyAsync(d_md, si + b_jobs, b.md.size(), hipMemcpyHostToDevice, stream);
+      if (e == hipSuccess) e = hipMemcpyAsync(d_jobs, si, b_jobs, hipMemcpyHostToDevice, stream);
       if (e == hipSuccess) {
         rc = mp3g_huffman_execute(device, d_jobs, n, d_md, d_gran, d_coef, stream);
         if (rc) return rc;
       }
     } else if (e == hipSuccess) {
-      e = hipMemcpyAsync(d_coef, b.coef.data(), b.coef.size() * sizeof(int16_t), hipMemcpyHostToDevice, stream);
+      std::memcpy(si, b.coef.data(), b_in);
+      e = hipMemcpyAsync(d_coef, si, b_in, hipMemcpyHostToDevice, stream);
     }
     if (e != hipSuccess) return abi_fail(MP3G_ERR_DEVICE, "decoder H2D copy");
+    lap(t_h2d);
     rc = mp3g_plan_execute(plan, d_gran, d_coef, d_state, d_state + 1, d_pcm, stream);
     if (rc) return rc;
+    lap(t_exec);
     e = hipMemcpyAsync(ahead.p, d_pcm, pcm_bytes, hipMemcpyDeviceToHost, stream);
+    lap(t_d2h);
     // carry: out -> in for the next batch
     if (e == hipSuccess) e = hipMemcpyAsync(d_state, d_state + 1, sizeof(mp3g_state), hipMemcpyDeviceToDevice, stream);
     if (e != hipSuccess) return abi_fail(MP3G_ERR_DEVICE, "decoder batch");
@@ -326,7 +511,9 @@ struct mp3g_decoder {
 
   // Waits for the batch on the device and makes it the served buffer.
   int complete(const Batch& b) {
+    const auto t0 = std::chrono::steady_clock::now();
     if (hipStreamSynchronize(stream) != hipSuccess) return abi_fail(MP3G_ERR_DEVICE, "decoder batch");
+    t_wait += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     std::swap(buf.p, ahead.p);
     std::swap(buf.n, ahead.n);
     std::swap(buf.cap, ahead.cap);
@@ -570,13 +757,26 @@ int mp3g_decoder_read(mp3g_decoder* d, uint8_t* out, size_t cap, size_t* n) {  /
 }
 
 int mp3g_decoder_read_full(mp3g_decoder* d, uint8_t* out, size_t cap, size_t* n) {  // io.ReadFull
+  // io.ReadFull loops Decoder.Read (one frame's PCM at most per call); the
+  // bytes it collects are the served PCM in order, so this copies whole spans
+  // of the served batch at once and leaves the frame index where the last of
+  // those Reads would (the frame holding the last byte copied).
   if (!d || !n || (cap && !out)) return abi_fail(MP3G_ERR_INVALID_ARGUMENT, "null argument");
   *n = 0;
   while (*n < cap) {
-    size_t k = 0;
-    const int rc = mp3g_decoder_read(d, out + *n, cap - *n, &k);
+    if (d->buf.size() - d->buf_off == 0) {
+      const int rc = d->refill();
+      if (rc != MP3G_OK) return rc;
+      continue;
+    }
+    const size_t k = std::min(cap - *n, d->buf.size() - d->buf_off);
+    const auto t0 = std::chrono::steady_clock::now();
+    std::memcpy(out + *n, d->buf.data() + d->buf_off, k);
+    d->t_copy += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    d->buf_off += k;
+    d->pos += (int64_t)k;
     *n += k;
-    if (rc != MP3G_OK) return rc;
+    while (d->next_end < d->frame_ends.size() && d->frame_ends[d->next_end] < d->buf_off) d->next_end++;
   }
   return MP3G_OK;
 }

@@ -216,9 +216,12 @@ std::vector<bool> g_pipe_busy;
 
 }  // namespace
 
+void release_pinned_pool();  // host_decoder.cpp: the decoders' pinned PCM pool
+
 extern "C" {
 
 void mp3g_release_cached_buffers(void) {
+  release_pinned_pool();
   std::lock_guard<std::mutex> lk(g_pipe_mu);
   int prev = -1;
   (void)hipGetDevice(&prev);

@@ -220,3 +220,31 @@ def test_corrupted_streams_statuses(gpu, sample_files):
                 break
         checked += 1
     assert checked > 10
+
+
+def _oracle_read_full(o, cap):
+    out = []
+    n = 0
+    while n < cap:
+        st, b = o.read(cap - n)
+        out.append(b)
+        n += len(b)
+        if st != oracle.ORC_OK:
+            return st, b"".join(out)
+    return oracle.ORC_OK, b"".join(out)
+
+
+@pytest.mark.parametrize("name", ["classic_lame.mp3", "mpeg2.mp3"])
+def test_read_full_spans_then_seek(gpu, sample_files, name):
+    """read_full copies whole spans of the served batch; the position and the
+    frame index it leaves must be those of the Reads it stands for: odd-sized
+    ReadFulls interleaved with relative / absolute seeks match the oracle's
+    Read loop byte for byte."""
+    d, o = both(gpu, sample_files[name])
+    buf = np.zeros(1 << 16, np.uint8)
+    for step, (cap, off, whence) in enumerate([(7777, 0, 1), (4608 * 3, -5000, 1), (12345, 4608 * 40 + 17, 0),
+                                               (4608, 2304, 1), (30000, -4608 * 7 - 3, 1), (9999, 0, 1)]):
+        st, k = d.read_full(buf[:cap])
+        st2, want = _oracle_read_full(o, cap)
+        assert st == ST[st2] and buf[:k].tobytes() == want, f"step {step}"
+        assert d.seek(off, whence) == o.seek(off, whence), f"step {step} seek"
