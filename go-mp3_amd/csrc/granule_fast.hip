@@ -35,6 +35,15 @@
 #include "dct4_18.h"
 #include "xlane.h"
 
+// timing-only builds (wrong PCM): drop the PCM stores / the coefficient or
+// line loads
+#ifndef MP3G_TIMING_NOSTORE
+#define MP3G_TIMING_NOSTORE 0
+#endif
+#ifndef MP3G_TIMING_NOLOAD
+#define MP3G_TIMING_NOLOAD 0
+#endif
+
 namespace mp3g {
 namespace v3 {
 // Independent chunks (one per wave) per workgroup, sharing the read-only
@@ -136,7 +145,8 @@ constexpr uint32_t kZones = 8;
 __device__ __forceinline__ void load_lines(const int16_t* coef, uint32_t g, int lane, uint32_t cw[9],
                                            int nbytes = (int)(MP3G_COEF_PER_GRANULE * sizeof(int16_t))) {
   const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<int16_t*>(coef + (size_t)g * MP3G_COEF_PER_GRANULE), (short)0, nbytes, 0x00020000);
+      const_cast<int16_t*>(coef + (size_t)g * MP3G_COEF_PER_GRANULE), (short)0, MP3G_TIMING_NOLOAD ? 0 : nbytes,
+      0x00020000);
   const int off = (lane >> 5) * 1152 + (lane & 31) * 36;
 #pragma unroll
   for (int i = 0; i < 3; i++) {
@@ -787,7 +797,7 @@ __device__ __forceinline__ void pack_pcm(const f2 acc2[9], int nch, uint32_t pk[
 // with no records (straight-line vmcnt accounting).
 __device__ __forceinline__ void store_pcm(int16_t* pcm, uint32_t g, bool out, const uint32_t pk[9], int hi, int k) {
   const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
-      pcm + (size_t)g * 1152, (short)0, out ? MP3G_PCM_BYTES_PER_GRANULE : 0, 0x00020000);
+      pcm + (size_t)g * 1152, (short)0, out && !MP3G_TIMING_NOSTORE ? MP3G_PCM_BYTES_PER_GRANULE : 0, 0x00020000);
 #pragma unroll
   for (int p = 0; p < 9; p++) __builtin_amdgcn_raw_buffer_store_b32(pk[p], rp, 4 * (32 * (2 * p + hi) + k), 0, 2);
 }
@@ -1428,7 +1438,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     {
       // issued for replayed granules too, through a resource with no records
       const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
-          pcm + (size_t)g * 1152, (short)0, out ? MP3G_PCM_BYTES_PER_GRANULE : 0, 0x00020000);
+          pcm + (size_t)g * 1152, (short)0, out && !MP3G_TIMING_NOSTORE ? MP3G_PCM_BYTES_PER_GRANULE : 0, 0x00020000);
 #pragma unroll
       for (int p = 0; p < 9; p++)
         __builtin_amdgcn_raw_buffer_store_b32(pk[p], rp, 4 * (32 * (2 * p + hi) + k), 0, 2);  // non-temporal: c2 -1.9 %, c3 -0.8 %

@@ -52,7 +52,8 @@ namespace {
 // touch no memory.
 __device__ __forceinline__ void synth_load(const float* lines, uint32_t g, uint32_t nbytes, int lane, f2 v[9]) {
   const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(lines + (size_t)g * MP3G_COEF_PER_GRANULE), (short)0, (int)nbytes, 0x00020000);
+      const_cast<float*>(lines + (size_t)g * MP3G_COEF_PER_GRANULE), (short)0, MP3G_TIMING_NOLOAD ? 0 : (int)nbytes,
+      0x00020000);
 #pragma unroll
   for (int r = 0; r < 9; r++) {
     const auto u = __builtin_amdgcn_raw_buffer_load_b64(rc, 8 * lane + 512 * r, 0, 0);
@@ -201,6 +202,13 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
   uint32_t pk[9] = {};  // PCM of a granule (stale for replayed ones: stored to no records)
   f2 A[9];
   load(w, A);
+#if !MP3G_SYNTH_NOPAD
+  // nine stores to no records, so that the loop is entered with the vector
+  // memory counter in the shape of its back edge (loads, then the PCM stores):
+  // without them the loads' waits at the loop top are placed for the entry
+  // path and also wait for the previous granule's stores, every granule
+  store_pcm(pcm, w, false, pk, hi, k);
+#endif
   wave_sync();
   const uint32_t span = end - w, span2 = 2 * span, span3 = 3 * span;
   for (uint32_t g = w; g < end; g++) {
@@ -251,7 +259,13 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
       for (int p = 0; p < 9; p++) acc2[p] = bcast(0.0f);
 #pragma unroll
       for (int v = -14; v <= 16; v += 2) {
+#if MP3G_SYNTH_RA1
+        int ia = (kHist + v) / 2;
+        asm volatile("" : "+v"(ia));
+        const f2 Av = RA[ia];
+#else
         const f2 Av = RA[(kHist + v) / 2];
+#endif
         const f2 Bv = {RB[kHist + v - 1], RB[kHist + v]};
 #pragma unroll
         for (int t = 0; t < 8; t++) {

@@ -196,29 +196,42 @@ MP3G_HD_INLINE void decode_sym(Reader<kSwap>& r, const uint16_t* T, uint32_t roo
   dox = d;
 }
 
-// 16-byte staging of consecutive line pairs (lines are produced strictly in
-// order from 0, two at a time).
+// Staging of consecutive line pairs into whole blocks of kBlk lines
+// (lines are produced strictly in order from 0, two at a time).  A block is
+// written by back-to-back 16-B stores of one lane: with 32-B blocks (the
+// default) every 32-B sector of the row is complete when it reaches the L2,
+// where 16-B blocks left half sectors that were written back to HBM as 32-B
+// requests twice (c3 write traffic 1.66x the coefficient bytes).
+#ifndef MP3G_HUFF_BLOCK_LINES
+#define MP3G_HUFF_BLOCK_LINES 16
+#endif
+constexpr int kBlk = MP3G_HUFF_BLOCK_LINES;  // 8, 16 or 32
+static_assert(kBlk == 8 || kBlk == 16 || kBlk == 32, "writer block");
 struct LineWriter {
   int16_t* row;
-  uint32_t b0, b1, b2, b3;
-  MP3G_HD_INLINE void put(int i, int a, int b) {
-    const uint32_t v = (uint32_t)(uint16_t)(int16_t)a | ((uint32_t)(uint16_t)(int16_t)b << 16);
-    const int slot = (i >> 1) & 3;
-    b0 = slot == 0 ? v : b0;
-    b1 = slot == 1 ? v : b1;
-    b2 = slot == 2 ? v : b2;
-    b3 = slot == 3 ? v : b3;
-    if (slot == 3) {
-      *reinterpret_cast<uint4*>(row + (i & ~7)) = make_uint4(b0, b1, b2, b3);
-      b0 = b1 = b2 = b3 = 0u;
+  uint32_t b[kBlk / 2];
+  MP3G_HD_INLINE void flush(int first) const {
+    uint4* d = reinterpret_cast<uint4*>(row + first);
+#pragma unroll
+    for (int q = 0; q < kBlk / 8; q++) d[q] = make_uint4(b[4 * q], b[4 * q + 1], b[4 * q + 2], b[4 * q + 3]);
+  }
+  MP3G_HD_INLINE void put(int i, int x, int y) {
+    const uint32_t v = (uint32_t)(uint16_t)(int16_t)x | ((uint32_t)(uint16_t)(int16_t)y << 16);
+    const int slot = (i >> 1) & (kBlk / 2 - 1);
+#pragma unroll
+    for (int q = 0; q < kBlk / 2; q++) b[q] = slot == q ? v : b[q];
+    if (slot == kBlk / 2 - 1) {
+      flush(i & ~(kBlk - 1));
+#pragma unroll
+      for (int q = 0; q < kBlk / 2; q++) b[q] = 0u;
     }
   }
-  // flushes the pending block (lines up to i, i even, then zeros to the next
-  // multiple of 8); returns that multiple of 8: the first line of the row
-  // left for the zero fill
+  // flushes the pending block (lines up to i, i even, then zeros to the end
+  // of the block); returns the first line after it: the first line of the
+  // row left for the zero fill (a multiple of 8)
   MP3G_HD_INLINE int finish(int i) {
-    if (i & 7) *reinterpret_cast<uint4*>(row + (i & ~7)) = make_uint4(b0, b1, b2, b3);
-    return (i + 7) & ~7;
+    if (i & (kBlk - 1)) flush(i & ~(kBlk - 1));
+    return (i + kBlk - 1) & ~(kBlk - 1);
   }
 };
 
@@ -299,7 +312,7 @@ MP3G_HD_INLINE int decode_job(const mp3g_hjob& job, uint64_t j, const uint64_t* 
   // (with a full vmcnt wait) in every loop iteration
   const mp3g_hjob J = job;
   int16_t* row = coef + j * MP3G_LINES;
-  LineWriter out{row, 0u, 0u, 0u, 0u};
+  LineWriter out{row, {}};
   if (J.sf_kind == MP3G_SF_NONE) {  // absent channel of a mono granule
     return 0;
   }
@@ -386,14 +399,14 @@ MP3G_HD_INLINE int decode_job(const mp3g_hjob& job, uint64_t j, const uint64_t* 
     const uint32_t root0 = s_root[J.table_select[0]], root1 = s_root[J.table_select[1]],
                    root2 = s_root[J.table_select[2]], qroot = s_root[32 + J.count1_table];
     const uint32_t lb0 = s_lin[J.table_select[0]], lb1 = s_lin[J.table_select[1]], lb2 = s_lin[J.table_select[2]];
-    // big values four pairs (one 16-B block) per step: the block's words sit
-    // in fixed registers (no per-pair slot select) and full blocks are stored
-    // straight away; the block holding bv2 (when it is not a multiple of 8)
-    // goes on in the writer for the count1 quads
-    for (int i0 = 0; i0 < bv2; i0 += 8) {
-      uint32_t w[4];
+    // big values one writer block (kBlk / 2 pairs) per step: the block's
+    // words sit in fixed registers (no per-pair slot select) and full blocks
+    // are stored straight away; the block holding bv2 (when it is not a
+    // multiple of kBlk) goes on in the writer for the count1 quads
+    for (int i0 = 0; i0 < bv2; i0 += kBlk) {
+      uint32_t w[kBlk / 2];
 #pragma unroll
-      for (int sl = 0; sl < 4; sl++) {
+      for (int sl = 0; sl < kBlk / 2; sl++) {
         const int ii = i0 + 2 * sl;
         w[sl] = 0u;
         if (ii < bv2) {
@@ -404,13 +417,12 @@ MP3G_HD_INLINE int decode_job(const mp3g_hjob& job, uint64_t j, const uint64_t* 
           w[sl] = (uint32_t)(uint16_t)(int16_t)a | ((uint32_t)(uint16_t)(int16_t)b << 16);
         }
       }
-      if (i0 + 8 <= bv2) {
-        *reinterpret_cast<uint4*>(row + i0) = make_uint4(w[0], w[1], w[2], w[3]);
-      } else {
-        out.b0 = w[0];
-        out.b1 = w[1];
-        out.b2 = w[2];
-        out.b3 = w[3];
+#pragma unroll
+      for (int sl = 0; sl < kBlk / 2; sl++) out.b[sl] = w[sl];
+      if (i0 + kBlk <= bv2) {
+        out.flush(i0);
+#pragma unroll
+        for (int sl = 0; sl < kBlk / 2; sl++) out.b[sl] = 0u;
       }
     }
     i = bv2;

@@ -26,8 +26,14 @@ d_l = torch.randn(n, 2, 576, device=dev, generator=gen) * 0.05
 d_p = torch.empty(n * 1152, dtype=torch.int16, device=dev)
 plan = mp3g.Plan(s, mode=mp3g.MODE_FAST)
 h = torch.cuda.current_stream().cuda_stream
-for _ in range(steps):
+for _ in range(2):
     plan.synth_execute(d_g, d_l, d_p, stream=h)
 torch.cuda.synchronize()
+ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+ev0.record()
+for _ in range(steps):
+    plan.synth_execute(d_g, d_l, d_p, stream=h)
+ev1.record()
+torch.cuda.synchronize()
 plan.close()
-print("done", steps)
+print("synth_only %s: %.4f ms per launch" % (os.path.basename(mp3g.lib_path()), ev0.elapsed_time(ev1) / steps))
