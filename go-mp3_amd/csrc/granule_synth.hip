@@ -39,6 +39,7 @@ constexpr int kSynthWaves = 8;
 #define MP3G_SYNTH_ABL 0
 #endif
 
+
 struct __align__(16) SynthWaveSmem {
   float ring[2][32][kSlots];
   uint32_t zone[kZones][2];  // hot zones of the chunk (record_hot)
@@ -155,10 +156,12 @@ __global__ void __launch_bounds__(kLanes * kSynthWaves, 4)
 granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, const mp3g_granule* __restrict__ gran,
                      const float* __restrict__ lines, const mp3g_state* __restrict__ state_in,
                      mp3g_state* __restrict__ state_out, int16_t* __restrict__ pcm) {
-  __shared__ __align__(16) float dwin_s[32][16];  // FastTables::dwin, pre-scaled by 32767
+  // FastTables::dwin, pre-scaled by 32767; rows padded to 20 floats, so the
+  // 16 lanes of a ds_read_b128 quad group hit 64 distinct banks
+  __shared__ __align__(16) float dwin_s[32][20];
   __shared__ SynthWaveSmem wsm[kSynthWaves];
   for (int e = threadIdx.x; e < 32 * 16; e += kLanes * kSynthWaves)
-    (&dwin_s[0][0])[e] = (&g_fast.dwin[0][0])[e] * 32767.0f;
+    dwin_s[e >> 4][e & 15] = (&g_fast.dwin[0][0])[e] * 32767.0f;
   __syncthreads();  // the only workgroup barrier
   const int lane = threadIdx.x & (kLanes - 1);
   const uint32_t ci = __builtin_amdgcn_readfirstlane(blockIdx.x * kSynthWaves + (threadIdx.x >> 6));
@@ -183,8 +186,7 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
     synth_load(lines, gg, nch * 2304u, lane, v);
   };
   const int hi = lane >> 5;
-  // the lane's 16 window taps, in registers for the whole chunk (read per
-  // granule they were four 4-way bank-conflicted ds_read_b128)
+  // the lane's 16 window taps, in registers for the whole chunk
   float dw[16];
   {
     const float4* d4 = reinterpret_cast<const float4*>(&dwin_s[k][0]);
@@ -200,34 +202,28 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
 
   uint32_t nz = 0;  // hot zones recorded (s.zone)
   uint32_t pk[9] = {};  // PCM of a granule (stale for replayed ones: stored to no records)
-  f2 A[9];
-  load(w, A);
-#if !MP3G_SYNTH_NOPAD
-  // nine stores to no records, so that the loop is entered with the vector
-  // memory counter in the shape of its back edge (loads, then the PCM stores):
-  // without them the loads' waits at the loop top are placed for the entry
-  // path and also wait for the previous granule's stores, every granule
-  store_pcm(pcm, w, false, pk, hi, k);
-#endif
-  wave_sync();
   const uint32_t span = end - w, span2 = 2 * span, span3 = 3 * span;
-  for (uint32_t g = w; g < end; g++) {
+  // one granule: stage buf (granule g), refill buf with granule gn, then the
+  // matrixing, window, PCM stores and history shift of g.  (A second buffer
+  // -- two granules in flight, the taps read from LDS per granule to stay at
+  // 116 VGPRs -- measured +1.5 % at c3: the loads are not latency-bound,
+  // DESIGN.md "Standalone polyphase kernel")
+  auto step = [&](uint32_t g, f2 (&buf)[9], uint32_t gn) {
     // progress-balanced issue priority, as in the fused kernel (c2 -3.5 %)
     const uint32_t left4 = 4u * (end - g);
     if (left4 > span3) __builtin_amdgcn_s_setprio(3);
     else if (left4 > span2) __builtin_amdgcn_s_setprio(2);
     else if (left4 > span) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
-    const uint32_t h = __builtin_amdgcn_readfirstlane(gran[g].header);
-    const int nch = hdr_nch(h);
+    const int nch = hdr_nch(__builtin_amdgcn_readfirstlane(gran[g].header));
     const bool out = g >= out_first;
     // a hot granule: its zone is redone in the reference's order after the pass
 #if MP3G_HOT_CHECK
-    const bool hot1 = __builtin_amdgcn_ballot_w64(max_abs_pairs(A) > kHotS) != 0;
+    const bool hot1 = __builtin_amdgcn_ballot_w64(max_abs_pairs(buf) > kHotS) != 0;
 #endif
-    if (!(MP3G_SYNTH_ABL & 1)) synth_stage(s, A, nch);
-    // the next granule in flight during the matrixing and window
-    load(g + 1, A);
+    if (!(MP3G_SYNTH_ABL & 1)) synth_stage(s, buf, nch);
+    // a later granule in flight during the matrixing and window
+    load(gn, buf);
     wave_sync();
 #if MP3G_HOT_CHECK
     // a hot granule (two tests, the second rare and on the staged S): its
@@ -259,13 +255,7 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
       for (int p = 0; p < 9; p++) acc2[p] = bcast(0.0f);
 #pragma unroll
       for (int v = -14; v <= 16; v += 2) {
-#if MP3G_SYNTH_RA1
-        int ia = (kHist + v) / 2;
-        asm volatile("" : "+v"(ia));
-        const f2 Av = RA[ia];
-#else
         const f2 Av = RA[(kHist + v) / 2];
-#endif
         const f2 Bv = {RB[kHist + v - 1], RB[kHist + v]};
 #pragma unroll
         for (int t = 0; t < 8; t++) {
@@ -287,7 +277,18 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
       for (int q = 0; q < 8; q++) col[q] = col[9 + q];
     }
     wave_sync();
-  }
+  };
+  // Loads are issued right after a granule is staged and waited for when it
+  // is staged; the preheader pads each buffer's loads with nine stores to no
+  // records, so that the loop is entered with the vector memory counter in the
+  // shape of its back edge (loads, then the PCM stores): without them the
+  // waits at the loop top are placed for the entry path and also wait for the
+  // previous granule's stores, every granule.
+  f2 A[9];
+  load(w, A);
+  store_pcm(pcm, w, false, pk, hi, k);
+  wave_sync();
+  for (uint32_t g = w; g < end; g++) step(g, A, g + 1);
 
   // vVec out; the IMDCT overlap `store` is not this stage's: passed through
   auto export_state = [&]() {
