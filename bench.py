@@ -180,12 +180,19 @@ def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle, pip
     # whose host scan overlaps the previous group's H2D, kernels and D2H
     # (the first call allocates its staging and device buffers, the second
     # reuses them: the time of the second)
-    pipe = []
+    # (its PCM is checked against the device leg's on a sample of granules:
+    # hp holds the device leg's PCM from the PCIe pass until the call below)
+    samp = np.unique(np.concatenate([np.arange(lo, min(lo + 256, n)) for lo in (0, n // 2, max(n - 256, 0))]))
+    samp_w = (samp[:, None] * 1152 + np.arange(1152)[None, :]).reshape(-1)
+    dev_pcm = hp[torch.from_numpy(samp_w)].clone()
+    pipe, pipe_same = [], None
     for _ in range(2 if pipelined else 0):
         t = time.perf_counter()
         n_p, _, st_p = mp3g.decode_streams_into(datas, hp, mode=mode, n_threads=16, device=idx)
         pipe.append(time.perf_counter() - t)
         assert n_p == n and all(x == 7 for x in st_p)
+        pipe_same = bool(torch.equal(hp[torch.from_numpy(samp_w)], dev_pcm))
+        assert pipe_same, "pipelined PCM differs from the device leg's"
     pipe_s = pipe[-1] if pipe else float("nan")
     mp3g.lib().mp3g_release_cached_buffers()
     # the io.Reader drop-in (mp3.NewDecoder + Read, decode.go:70-80, 361-388)
@@ -197,13 +204,16 @@ def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle, pip
     rbuf = np.empty(1 << 20, np.uint8)
     dec_data = datas[0] if cfg == "c2" else synth.encode_stream(seed0, 10000)  # the c2 stream
     dec_times = []
-    got_bytes, st_r = 0, None
+    got_bytes, st_r, dec_same = 0, None, None
     for _ in range(2 if pipelined else 0):
         t = time.perf_counter()
         got_bytes, st_r = 0, None
         dec = mp3g.Decoder(dec_data, mode=mode, device=idx)
         while True:
             st_r, k = dec.read_full(rbuf)  # io.ReadFull: Read until 1 MiB (Read gives <= 1 frame)
+            if got_bytes == 0 and cfg == "c2" and pipe:  # c2: the same stream as the pipelined leg
+                dec_same = bool(np.array_equal(rbuf[:k], hp.view(torch.uint8)[:k].numpy()))
+                assert dec_same, "Decoder PCM differs from the pipelined leg's"
             got_bytes += k
             if st_r != 0:
                 break
@@ -231,6 +241,7 @@ def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle, pip
            # sum of the host scan and the PCIe-inclusive device leg
            "end_to_end": {"frames_per_s": round(frames / pipe_s, 1) if pipe else None,
                           "pipelined_s": round(pipe_s, 4) if pipe else None,
+                          "pcm_equals_device_leg_sample": pipe_same,
                           "api": "mp3g_decode_streams_into (16 host threads, pinned PCM out)",
                           "serial_frames_per_s": round(frames / (scan_s + pcie_s), 1),
                           "host_scan_s": round(scan_s, 4), "h2d_huffman_dsp_d2h_s": round(pcie_s, 4),
@@ -241,7 +252,8 @@ def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle, pip
                                   "(the c2 bitstream: 10,000 frames)",
                            "first_decoder_s": round(dec_times[0], 4),
                            "note": "the second decoder of the process (pinned / device buffers pooled by the library)",
-                           "read_status": int(st_r)}}
+                           "read_status": int(st_r),
+                           "first_block_equals_pipelined": dec_same}}
     if check_oracle:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
         import oracle  # parity check of the timed output (checker only)

@@ -43,6 +43,10 @@
 #ifndef MP3G_TIMING_NOLOAD
 #define MP3G_TIMING_NOLOAD 0
 #endif
+// cache policy of the PCM stores (2 = nt: streamed past the caches)
+#ifndef MP3G_PCM_STORE_AUX
+#define MP3G_PCM_STORE_AUX 2
+#endif
 
 namespace mp3g {
 namespace v3 {
@@ -799,7 +803,8 @@ __device__ __forceinline__ void store_pcm(int16_t* pcm, uint32_t g, bool out, co
   const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
       pcm + (size_t)g * 1152, (short)0, out && !MP3G_TIMING_NOSTORE ? MP3G_PCM_BYTES_PER_GRANULE : 0, 0x00020000);
 #pragma unroll
-  for (int p = 0; p < 9; p++) __builtin_amdgcn_raw_buffer_store_b32(pk[p], rp, 4 * (32 * (2 * p + hi) + k), 0, 2);
+  for (int p = 0; p < 9; p++)
+    __builtin_amdgcn_raw_buffer_store_b32(pk[p], rp, 4 * (32 * (2 * p + hi) + k), 0, MP3G_PCM_STORE_AUX);
 }
 
 // Entry state of a replay start: overlap store in registers, V history as X
