@@ -36,7 +36,7 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 METRIC = "MP3 frames/sec (44.1 kHz stereo 128 kbps) at 1/2/4/8 GPUs; max |ΔPCM| LSB"
 
 
-MODES = {"exact": ("exact (bit-exact vs reference)", "mp3g::v2::granule_fused_kernel"),
+MODES = {"exact": ("exact (bit-exact vs reference)", "mp3g::v4::granule_wexact_kernel"),
          "fast": ("fast (+-1 LSB vs reference)", "mp3g::v3::granule_fast_kernel")}
 
 

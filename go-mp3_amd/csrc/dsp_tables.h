@@ -76,6 +76,12 @@ struct FastTables {
   // reference's summation order -- nrow[m] = synthNWin[m-16] (m >= 16),
   // -synthNWin[48-m] (m < 16), negated rows giving bit-negated sums
   float nrow[32][32];
+  // exact mode (v4, granule_wexact.hip) also carries V[16], the residue of
+  // synthNWin's row 16 (~1e-16, not zero: tests/test_tables.py): that row and
+  // the synthesis-window taps of output 16 that read it (synthDtbl[32 j + 16],
+  // j even)
+  float nrow16[32];
+  float dwin16[8];
   float aa_cs[8], aa_ca[8];
   float is_ratio[8][2];           // [is_pos][ch] (rows 0..6 used)
   // per (combo, output line L): the line's long band (bits 0..4), short band

@@ -161,6 +161,38 @@ __device__ __forceinline__ void load_lines(const int16_t* coef, uint32_t g, int 
   }
 }
 
+// The same, reading only the lines below `lim` (the lane's channel's count1;
+// 0 for a channel the granule does not have): lines >= count1 are zero (the
+// bitstream parse's guarantee, maindata/huffman.go:127-134, which mp3g_validate
+// checks), so a 6-line piece starting at or above it is not fetched -- its
+// offset is pushed past the records and the load returns 0 without touching
+// memory.  At 128 kbps about 40 % of the coefficient bytes are skipped.
+constexpr int kNoRecord = 0x40000000;
+__device__ __forceinline__ void load_lines_lim(const int16_t* coef, uint32_t g, int lane, uint32_t cw[9], int nbytes,
+                                               int lim) {
+  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<int16_t*>(coef + (size_t)g * MP3G_COEF_PER_GRANULE), (short)0, MP3G_TIMING_NOLOAD ? 0 : nbytes,
+      0x00020000);
+  const int l0 = 18 * (lane & 31);
+  const int off = (lane >> 5) * 1152 + 2 * l0;
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b96(rc, l0 + 6 * i < lim ? off + 12 * i : kNoRecord, 0, 0);
+    cw[3 * i] = v[0];
+    cw[3 * i + 1] = v[1];
+    cw[3 * i + 2] = v[2];
+  }
+}
+#ifndef MP3G_FAST_SKIP_ZERO
+#define MP3G_FAST_SKIP_ZERO 0
+#endif
+// the line limit of lane (ch, sb) in granule g (wave-uniform g: scalar loads)
+__device__ __forceinline__ int count1_lim(const mp3g_granule* gran, uint32_t g, int lane) {
+  const uint32_t h = gran[g].header;
+  const int c0 = gran[g].ch[0].count1, c1 = gran[g].ch[1].count1;
+  return (lane >> 5) ? (common::hdr_nch(h) == 2 ? c1 : 0) : c0;
+}
+
 // Replay start of a chunk (same decision as v2::plan_prologue, with wave
 // ballots instead of a workgroup scan).
 __device__ void prologue(const ChunkDesc& cd, const mp3g_granule* gran, uint64_t* w_out, int init_in[2],
@@ -334,6 +366,15 @@ __device__ __forceinline__ const float* vtab(const float* p) {
   asm volatile("" : "+s"(p));
   return p;
 }
+// The same for tables every lane reads at the same index: a constant-address-
+// space pointer, so the reads are scalar loads (SGPR operands), not vector
+// loads into ~hundreds of VGPRs.
+typedef const float __attribute__((address_space(4))) cfloat4;
+__device__ __forceinline__ cfloat4* stab(const float* p) {
+  cfloat4* q = (cfloat4*)p;
+  asm volatile("" : "+s"(q));
+  return q;
+}
 
 // The per-slot test on S in the ring's current slots (wave-uniform).
 __device__ __forceinline__ bool slot_sums_hot(const float (&ring)[2][32][kSlots], int nch) {
@@ -474,7 +515,8 @@ struct GranParams {
 
 // Reads the descriptor in s.desc and fills the band exponents s.expo (long
 // bands only when no channel has short blocks).
-__device__ __forceinline__ GranParams granule_params(WaveSmem& s, int ch) {
+template <class WS>
+__device__ __forceinline__ GranParams granule_params(WS& s, int ch) {
   GranParams P;
   // wave-uniform (SGPR): the per-combo tables become scalar loads
   P.h = __builtin_amdgcn_readfirstlane(s.desc.header);
@@ -521,7 +563,8 @@ __device__ __forceinline__ GranParams granule_params(WaveSmem& s, int ch) {
 
 // Requantization of long-block granules, lane = (ch, sb = k), from the raw
 // lines in registers.
-__device__ __forceinline__ void front_long_fast(float x[18], const uint32_t cw[9], const WaveSmem& s,
+template <class WS>
+__device__ __forceinline__ void front_long_fast(float x[18], const uint32_t cw[9], const WS& s,
                                                 const SharedSmem& sh, const GranParams& P, int ch, int k) {
   int xi[18];
 #pragma unroll
@@ -549,8 +592,8 @@ __device__ __forceinline__ void front_long_fast(float x[18], const uint32_t cw[9
 // Requantization in gather form (any block type; the reorder of short
 // blocks, frame.go:184-302): the channel's raw lines staged in the current
 // slots of the ring, lane (ch, sb) gathering its 18 output lines.
-template <bool kExact>
-__device__ __forceinline__ void front_gather(float x[18], const uint32_t cw[9], WaveSmem& s, const GranParams& P,
+template <bool kExact, class WS>
+__device__ __forceinline__ void front_gather(float x[18], const uint32_t cw[9], WS& s, const GranParams& P,
                                              int ch, int k) {
   int nsfs = 0;  // short bands whose first line lies below count1 (frame.go:229-255 loop bound)
 #pragma unroll
@@ -591,7 +634,8 @@ __device__ __forceinline__ void front_gather(float x[18], const uint32_t cw[9], 
 
 // MS / intensity stereo with the partner channel's lane (frame.go:304-420):
 // single roundings in the reference's order, exact in both modes.
-__device__ __forceinline__ void stereo_stage(float x[18], const WaveSmem& s, const SharedSmem& sh,
+template <class WS, class SH>
+__device__ __forceinline__ void stereo_stage(float x[18], const WS& s, const SH& sh,
                                              const GranParams& P, int ch) {
   if (!(P.nch == 2 && hdr_mode(P.h) == 1 && (P.h & 0x30u))) return;
   const mp3g_channel& C0 = s.desc.ch[0];
@@ -834,7 +878,7 @@ __device__ __forceinline__ void init_state(WaveSmem& s, const mp3g_state* sin, c
 // The granule's descriptor into s.desc and its lines into cw (direct loads).
 __device__ __forceinline__ void load_granule(const mp3g_granule* gran, const int16_t* coef, uint32_t g, int lane,
                                              WaveSmem& s, uint32_t cw[9]) {
-  load_lines(coef, g, lane, cw);
+  load_lines_lim(coef, g, lane, cw, (int)(MP3G_COEF_PER_GRANULE * sizeof(int16_t)), count1_lim(gran, g, lane));
   if (lane < 10) reinterpret_cast<uint4*>(&s.desc)[lane] = reinterpret_cast<const uint4*>(gran + g)[lane];
 }
 
@@ -1001,7 +1045,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
 
   uint32_t cw[9] = {};  // the current granule's raw coefficients (lane's 18 lines)
   if (w < end) {
-    load_lines(coef, w, lane, cw);
+    load_lines_lim(coef, w, lane, cw, (int)(MP3G_COEF_PER_GRANULE * sizeof(int16_t)), count1_lim(gran, w, lane));
     if (lane < 10) reinterpret_cast<uint4*>(&s.desc)[lane] = reinterpret_cast<const uint4*>(gran + w)[lane];
   }
   wave_sync();
@@ -1031,6 +1075,13 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       else __builtin_amdgcn_s_setprio(0);
     }
     const bool out = g >= out_first;
+#if MP3G_FAST_SKIP_ZERO
+    // the next granule's channel count and count1s for its prefetch: scalar
+    // loads issued here, long before the prefetch below needs them
+    const uint32_t gq = g + 1 < end ? g + 1 : g;
+    const uint32_t nx_h = gran[gq].header;
+    const uint32_t nx_c0 = gran[gq].ch[0].count1, nx_c1 = gran[gq].ch[1].count1;
+#endif
     // does a replayed granule's V feed anything? (see v2 / DESIGN.md halo)
     bool need_v = true;
     if (!out && g + 1 < out_first) need_v = hdr_nch(gran[g + 1].header) < hdr_nch(s.desc.header);
@@ -1333,7 +1384,12 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     // issued unconditionally (straight-line vmcnt accounting, as the PCM
     // stores below): past the chunk the resources have no records
     {
+#if MP3G_FAST_SKIP_ZERO
+      const int lim = ch ? (hdr_nch(nx_h) == 2 ? (int)nx_c1 : 0) : (int)nx_c0;
+      load_lines_lim(coef, g + 1, lane, cw, more ? (int)(MP3G_COEF_PER_GRANULE * sizeof(int16_t)) : 0, lim);
+#else
       load_lines(coef, g + 1, lane, cw, more ? (int)(MP3G_COEF_PER_GRANULE * sizeof(int16_t)) : 0);
+#endif
       if (lane < 10) {
         const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<mp3g_granule*>(gran + g + 1), (short)0, more ? (int)sizeof(mp3g_granule) : 0, 0x00020000);

@@ -28,11 +28,14 @@ static_assert(sizeof(ChunkDesc) == 32, "ChunkDesc layout");
 // Host-side launchers (defined next to the kernels; no RDC needed).
 hipError_t upload_tables(const DspTables& tables);
 // Exact-mode kernel variants: v1 = per-phase reference implementation,
-// v2 = fused/register-blocked production kernel (default).
+// v2 = fused/register-blocked workgroup kernel (both kept as cross-checks:
+// MP3G_FLAG_KERNEL_V1 / _V2), v4 = one wave per chunk (default).
 constexpr int kVariantV1 = 1;
 constexpr int kVariantV2 = 2;
 // fast mode (MP3G_MODE_FAST): one wave per chunk, reassociated transforms, +-1 LSB
 constexpr int kVariantFast = 3;
+// exact mode v4 (default): one wave per chunk, the reference's operation order
+constexpr int kVariantExact4 = 4;
 hipError_t launch_granule(int variant, const ChunkDesc* d_chunks, uint32_t n_chunks,
                           const mp3g_granule* d_gran, const int16_t* d_coef,
                           const mp3g_state* d_state_in, mp3g_state* d_state_out, int16_t* d_pcm,
@@ -63,6 +66,12 @@ hipError_t fast_kernel_attributes(hipFuncAttributes* a, int* waves_per_block);
 hipError_t launch_fast(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_granule* d_gran,
                        const int16_t* d_coef, const mp3g_state* d_state_in, mp3g_state* d_state_out,
                        int16_t* d_pcm, unsigned long long* d_stamps, hipStream_t stream);
+
+// Exact mode v4 (granule_wexact.hip, same TU as the fast kernel).
+hipError_t wexact_kernel_attributes(hipFuncAttributes* a, int* waves_per_block);
+hipError_t launch_wexact(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_granule* d_gran,
+                         const int16_t* d_coef, const mp3g_state* d_state_in, mp3g_state* d_state_out,
+                         int16_t* d_pcm, hipStream_t stream);
 
 // Standalone polyphase synthesis (granule_synth.hip, same TU): float32
 // frequency-inverted lines [n][2][576] -> s16 PCM, over a fast-mode plan.

@@ -1,10 +1,10 @@
 // kernels.hip -- device translation unit of the exact-mode and main-data
 // kernels of libmp3g.so.
 //
-// Holds their constant tables (uploaded once per device) and both exact-mode
-// kernels: v1 (granule_exact.hip, the straightforward per-phase version, kept
-// as an on-device cross-check) and v2 (granule_fused.hip, the production
-// kernel), and the main-data (scale factor + Huffman) kernel
+// Holds their constant tables (uploaded once per device), the workgroup
+// exact-mode kernels v1 (granule_exact.hip, the straightforward per-phase
+// version) and v2 (granule_fused.hip), both kept as on-device cross-checks of
+// the default exact kernel v4 (kernels_fast.hip), and the main-data (scale factor + Huffman) kernel
 // (huffman_dev.hip).  One TU so they reach g_tab / g_huff without
 // relocatable device code.  The fast-mode kernel v3 has a TU of its own
 // (kernels_fast.hip: its own table copy g_fast and codegen options).
@@ -51,8 +51,11 @@ int chunks_per_cu(int variant) {
   hipFuncAttributes a;
   hipError_t e;
   int waves_per_block;
+  const bool per_wave = variant == kVariantFast || variant == kVariantExact4;
   if (variant == kVariantFast) {
     e = fast_kernel_attributes(&a, &waves_per_block);
+  } else if (variant == kVariantExact4) {
+    e = wexact_kernel_attributes(&a, &waves_per_block);
   } else if (variant == kVariantV1) {
     e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&v1::granule_exact_kernel));
     waves_per_block = 4;
@@ -68,7 +71,7 @@ int chunks_per_cu(int variant) {
   int blocks = waves_per_simd * 4 / waves_per_block;
   if (a.sharedSizeBytes > 0) blocks = std::min<int>(blocks, (int)(163840 / a.sharedSizeBytes));
   blocks = std::max(blocks, 1);
-  return variant == kVariantFast ? blocks * waves_per_block : blocks;
+  return per_wave ? blocks * waves_per_block : blocks;
 }
 
 hipError_t launch_granule(int variant, const ChunkDesc* d_chunks, uint32_t n_chunks,
@@ -78,7 +81,9 @@ hipError_t launch_granule(int variant, const ChunkDesc* d_chunks, uint32_t n_chu
   if (n_chunks == 0) return hipSuccess;
   if (variant == kVariantFast)
     return launch_fast(d_chunks, n_chunks, d_gran, d_coef, d_state_in, d_state_out, d_pcm, nullptr, stream);
-  else if (variant == kVariantV1)
+  if (variant == kVariantExact4)
+    return launch_wexact(d_chunks, n_chunks, d_gran, d_coef, d_state_in, d_state_out, d_pcm, stream);
+  if (variant == kVariantV1)
     hipLaunchKernelGGL(v1::granule_exact_kernel, dim3(n_chunks), dim3(256), 0, stream, d_chunks,
                        d_gran, d_coef, d_state_in, d_state_out, d_pcm);
   else

@@ -1,5 +1,8 @@
-// kernels_fast.hip -- device translation unit of the fast-mode granule kernel
-// (v3, granule_fast.hip, MP3G_MODE_FAST) with its own copy of the fast tables.
+// kernels_fast.hip -- device translation unit of the one-wave-per-chunk
+// granule kernels: fast mode v3 (granule_fast.hip, MP3G_MODE_FAST), the
+// standalone polyphase kernel (granule_synth.hip) and exact mode v4
+// (granule_wexact.hip, the default MP3G_MODE_EXACT kernel), with their own
+// copy of the fast tables.
 //
 // Own TU so it gets its own codegen options (Makefile): it is compiled with
 // machine LICM off.  The kernel's packed-FP32 transforms take their constants
@@ -27,6 +30,7 @@ __device__ float g_req[4][8207];
 #include "granule_hdr.h"
 #include "granule_fast.hip"
 #include "granule_synth.hip"
+#include "granule_wexact.hip"
 
 namespace mp3g {
 
@@ -52,6 +56,21 @@ hipError_t launch_fast(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_
   else
     hipLaunchKernelGGL(v3::granule_fast_kernel<false>, grid, block, 0, stream, d_chunks, n_chunks, d_gran, d_coef,
                        d_state_in, d_state_out, d_pcm, nullptr);
+  return hipGetLastError();
+}
+
+hipError_t wexact_kernel_attributes(hipFuncAttributes* a, int* waves_per_block) {
+  *waves_per_block = v4::kXWaves;
+  return hipFuncGetAttributes(a, reinterpret_cast<const void*>(&v4::granule_wexact_kernel));
+}
+
+hipError_t launch_wexact(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_granule* d_gran,
+                         const int16_t* d_coef, const mp3g_state* d_state_in, mp3g_state* d_state_out,
+                         int16_t* d_pcm, hipStream_t stream) {
+  if (n_chunks == 0) return hipSuccess;
+  const dim3 grid((n_chunks + v4::kXWaves - 1) / v4::kXWaves), block(64 * v4::kXWaves);
+  hipLaunchKernelGGL(v4::granule_wexact_kernel, grid, block, 0, stream, d_chunks, n_chunks, d_gran, d_coef,
+                     d_state_in, d_state_out, d_pcm);
   return hipGetLastError();
 }
 

@@ -91,14 +91,23 @@ int ensure_device(int dev) {
 // faster than k = 8) and ~64 granules for c3 (4 % faster than k = 256, 20 %
 // faster than one round of 683-granule chunks; sweeps measured on MI355X,
 // tools/gpu_chunks.sh).
-uint32_t auto_chunk(const mp3g_stream* streams, uint32_t n_streams, int device, uint32_t base_mode) {
+// The granule kernel a plan's mode runs: fast v3, or exact v4 unless a
+// cross-check kernel is asked for (MP3G_FLAG_KERNEL_V1 / _V2).
+int plan_variant(uint32_t mode) {
+  if ((mode & 0xffu) == MP3G_MODE_FAST) return kVariantFast;
+  if (mode & MP3G_FLAG_KERNEL_V1) return kVariantV1;
+  if (mode & MP3G_FLAG_KERNEL_V2) return kVariantV2;
+  return kVariantExact4;
+}
+
+uint32_t auto_chunk(const mp3g_stream* streams, uint32_t n_streams, int device, uint32_t mode) {
   uint64_t maxn = 0;
   for (uint32_t s = 0; s < n_streams; s++) maxn = std::max<uint64_t>(maxn, streams[s].n_granules);
   if (maxn == 0) return 1;
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
   const uint64_t resident =
-      (uint64_t)cus * (uint64_t)chunks_per_cu(base_mode == MP3G_MODE_FAST ? kVariantFast : kVariantV2);
+      (uint64_t)cus * (uint64_t)chunks_per_cu(plan_variant(mode));
   uint64_t best_k = 1;
   double best = 0.0;
   for (uint64_t k = 1; k <= maxn;) {
@@ -136,14 +145,14 @@ std::vector<uint64_t> spread_chunks(const mp3g_stream* streams, uint32_t n_strea
 // model's 3,334 chunks put 4 workgroups on 66 CUs and 3 on the others, and
 // the 4-workgroup CUs set the launch time) and the streams are cut into
 // chunks of equal length.
-std::vector<uint64_t> auto_chunks(const mp3g_stream* streams, uint32_t n_streams, int device, uint32_t base_mode) {
-  const uint64_t k = auto_chunk(streams, n_streams, device, base_mode);
+std::vector<uint64_t> auto_chunks(const mp3g_stream* streams, uint32_t n_streams, int device, uint32_t mode) {
+  const uint64_t k = auto_chunk(streams, n_streams, device, mode);
   uint64_t c0 = 0;
   for (uint32_t s = 0; s < n_streams; s++) c0 += (streams[s].n_granules + k - 1) / k;
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus <= 0) cus = 256;
   const uint64_t resident =
-      (uint64_t)cus * (uint64_t)chunks_per_cu(base_mode == MP3G_MODE_FAST ? kVariantFast : kVariantV2);
+      (uint64_t)cus * (uint64_t)chunks_per_cu(plan_variant(mode));
   if (2 * c0 < resident) {
     std::vector<uint64_t> c(n_streams);
     for (uint32_t s = 0; s < n_streams; s++) c[s] = (streams[s].n_granules + k - 1) / k;
@@ -252,9 +261,11 @@ int mp3g_plan_create(int device, const mp3g_stream* streams, uint32_t n_streams,
   if (base_mode != MP3G_MODE_EXACT && base_mode != MP3G_MODE_FAST)
     return fail(MP3G_ERR_UNSUPPORTED, "mode not available");
   for (uint32_t s = 0; s < n_streams; s++) {
-    // the fast kernel indexes granules with 32-bit wave-uniform scalars
-    if (base_mode == MP3G_MODE_FAST && streams[s].first_granule + streams[s].n_granules >= (1ull << 32))
-      return fail(MP3G_ERR_UNSUPPORTED, "fast mode: granule index >= 2^32");
+    // the one-wave kernels (fast v3, exact v4) index granules with 32-bit
+    // wave-uniform scalars
+    const int v = plan_variant(mode);
+    if ((v == kVariantFast || v == kVariantExact4) && streams[s].first_granule + streams[s].n_granules >= (1ull << 32))
+      return fail(MP3G_ERR_UNSUPPORTED, "granule index >= 2^32 (use MP3G_FLAG_KERNEL_V2 in exact mode)");
   }
   DeviceGuard guard(device);
   if (guard.err != hipSuccess) return fail(MP3G_ERR_NO_DEVICE, "hipSetDevice", guard.err);
@@ -263,7 +274,7 @@ int mp3g_plan_create(int device, const mp3g_stream* streams, uint32_t n_streams,
   // chunks per stream (lengths within a stream differ by at most one)
   std::vector<uint64_t> nc;
   if (granules_per_chunk == 0) {
-    nc = auto_chunks(streams, n_streams, device, base_mode);
+    nc = auto_chunks(streams, n_streams, device, mode);
   } else if (granules_per_chunk & 0x80000000u) {
     nc = spread_chunks(streams, n_streams, std::max<uint32_t>(1, granules_per_chunk & 0x7fffffffu));
   } else {
@@ -356,10 +367,7 @@ int mp3g_plan_execute(mp3g_plan* p, const mp3g_granule* d_gran, const int16_t* d
   for (const ChunkDesc& c : p->chunks) {
     if ((c.flags & kChunkStateOut) && !d_state_out) return fail(MP3G_ERR_INVALID_ARGUMENT, "state_out needed");
   }
-  const int variant = (p->mode & 0xffu) == MP3G_MODE_FAST ? kVariantFast
-                      : (p->mode & MP3G_FLAG_KERNEL_V1)      ? kVariantV1
-                                                             : kVariantV2;
-  HIP_TRY(launch_granule(variant, p->d_chunks, (uint32_t)p->chunks.size(), d_gran, d_coef, d_state_in,
+  HIP_TRY(launch_granule(plan_variant(p->mode), p->d_chunks, (uint32_t)p->chunks.size(), d_gran, d_coef, d_state_in,
                          d_state_out, d_pcm, static_cast<hipStream_t>(hip_stream)));
   return MP3G_OK;
 }

@@ -14,7 +14,7 @@ import time
 import numpy as np
 
 __all__ = ["CHANNEL_DTYPE", "GRANULE_DTYPE", "STREAM_DTYPE", "STATE_DTYPE", "MODE_EXACT",
-           "MODE_FAST", "FLAG_CHECKED", "FLAG_KERNEL_V1", "FLAG_HOST_HUFFMAN", "STATE_IN", "STATE_OUT", "Mp3gError", "lib", "lib_path",
+           "MODE_FAST", "FLAG_CHECKED", "FLAG_KERNEL_V1", "FLAG_KERNEL_V2", "FLAG_HOST_HUFFMAN", "STATE_IN", "STATE_OUT", "Mp3gError", "lib", "lib_path",
            "decode_host", "validate", "Plan", "device_count", "streams_for", "parse_stream",
            "parse_streams", "Decoder", "HJOB_DTYPE", "scan_streams", "huffman_execute", "decode_streams"]
 
@@ -39,6 +39,7 @@ assert CHANNEL_DTYPE.itemsize == 72 and GRANULE_DTYPE.itemsize == 160 and HJOB_D
 assert STREAM_DTYPE.itemsize == 16 and STATE_DTYPE.itemsize == 12800
 
 MODE_EXACT, MODE_FAST, FLAG_CHECKED, FLAG_KERNEL_V1, FLAG_HOST_HUFFMAN = 0, 1, 0x100, 0x200, 0x400
+FLAG_KERNEL_V2 = 0x800  # exact mode via the workgroup v2 kernel (cross-check of the default v4)
 STATE_IN, STATE_OUT = 1, 2
 MP3G_PCM_BYTES_PER_GRANULE = 2304  # include/mp3g.h: 576 stereo s16 samples
 

@@ -100,7 +100,11 @@ typedef struct mp3g_granule {
 
 /* ---- cross-granule DSP state (reference Frame.store / Frame.vVec) ------- */
 /* Layout identical to the reference fields (frame.go:48-49): copying a
- * Frame's state in/out is a memcpy.  12,800 bytes. */
+ * Frame's state in/out is a memcpy.  12,800 bytes.  A state_in is a state a
+ * decoder produced (Frame.store / vVec are only ever written by Decode): its
+ * vVec blocks are V = synthNWin * S, whose 64 entries hold 33 distinct values,
+ * and the one-wave kernels (fast v3, exact v4) keep only those; the workgroup
+ * kernels (MP3G_FLAG_KERNEL_V1 / _V2) carry all 64 of any vvec. */
 typedef struct mp3g_state {
   float store[2][32][18]; /* IMDCT overlap                          */
   float vvec[2][1024];    /* polyphase FIFO, newest V block at [0:64] */
@@ -125,6 +129,8 @@ typedef struct mp3g_stream {
 #define MP3G_MODE_FAST  1u   /* MFMA/fast-transform polyphase; |dPCM| <= 1 LSB          */
 #define MP3G_FLAG_CHECKED 0x100u /* validate descriptor ranges on the host first      */
 #define MP3G_FLAG_KERNEL_V1 0x200u /* exact mode via the per-phase v1 kernel (cross-check) */
+#define MP3G_FLAG_KERNEL_V2 0x800u /* exact mode via the workgroup v2 kernel (cross-check; the
+                                      default exact kernel is v4, one wave per chunk) */
 #define MP3G_FLAG_HOST_HUFFMAN 0x400u /* decoder: scale factors + Huffman on the host (mp3g_parse_*)
                                          instead of the GPU main-data kernel (cross-check) */
 

@@ -147,10 +147,13 @@ def test_edge_cases(gpu):
         assert_pcm_equal(pcm, want, name)
     assert np.all(gpu.decode_host(g0, c0, s)[0] == 0)
     assert np.abs(gpu.decode_host(g1, c1, s)[0]).max() == 32767
-    # empty streams interleaved with real ones, state export of an empty stream
-    st_in = np.zeros(3, gpu.STATE_DTYPE)
-    st_in["store"] = rng.standard_normal(st_in["store"].shape).astype(np.float32)
-    st_in["vvec"] = rng.standard_normal(st_in["vvec"].shape).astype(np.float32)
+    # empty streams interleaved with real ones, state export of an empty stream;
+    # state_in is a decoder's state (Frame.store / vVec are only ever produced by
+    # Decode itself, frame.go:42-50): the exported states of three other streams
+    gp, cp, sp = synth.synth_batch(3, 7, seed=11, p_event=0.2)
+    sp["flags"] = gpu.STATE_OUT
+    _, st_in = oracle.dsp_streams(gp, cp, sp)
+    assert np.abs(st_in["vvec"]).max() > 0
     streams = np.zeros(3, gpu.STREAM_DTYPE)
     streams["first_granule"] = [0, 0, 0]
     streams["n_granules"] = [0, n, 0]
@@ -195,10 +198,11 @@ def test_c3_shape_bit_exact_and_batch_invariance(gpu):
     assert_pcm_equal(np.concatenate([p_a, p_b]), want, "c3 split batches")
 
 
-@pytest.mark.parametrize("variant", ["v1", "v2"])
+@pytest.mark.parametrize("variant", ["v1", "v2", "v4"])
 def test_kernel_variants_agree(gpu, captured, variant):
-    """Both exact kernels (per-phase v1, fused v2) are bit-exact on every case."""
-    mode = gpu.FLAG_KERNEL_V1 if variant == "v1" else 0
+    """Every exact kernel (per-phase v1, workgroup v2, one-wave v4 = the
+    default) is bit-exact on every case."""
+    mode = {"v1": gpu.FLAG_KERNEL_V1, "v2": gpu.FLAG_KERNEL_V2, "v4": 0}[variant]
     g, c, want = captured["classic_lame.mp3"]
     pcm, _ = run_plan(gpu, g, c, gpu.streams_for([len(g)]), chunk=7, mode=mode)
     assert_pcm_equal(pcm, want, variant)

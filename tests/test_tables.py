@@ -122,3 +122,29 @@ def test_imdct36_symmetries(tabs):
         assert np.array_equal(c[:, 17 - p], -c[:, p])
     for p in range(18, 27):
         assert np.array_equal(c[:, 53 - p], c[:, p])
+
+
+def _inc_table(text, name, shape):
+    import re
+    body = text.split(f"{name}{''.join(f'[{d}]' for d in shape)} = {{", 1)[1].split("};", 1)[0]
+    vals = [float.fromhex(v.rstrip("f")) for v in re.findall(r"-?0x[0-9a-fA-Fp.+-]+f", body)]
+    return np.array(vals, dtype=np.float64).astype(np.float32).reshape(shape)
+
+
+def test_exact_kernel_literals(tabs):
+    """The v4 exact kernel's instruction literals (go-mp3_amd/csrc/exact_consts.inc,
+    generated from the library's dsp_tables.cpp) are the reference's float32
+    tables: cosN36's distinct columns, cosN12, and the synthNWin rows of the
+    32 distinct V values (negated rows 33..48 for X[1..15], X[0] = -row 48) +
+    row 16."""
+    import os
+    text = open(os.path.join(os.path.dirname(__file__), "..", "go-mp3_amd", "csrc", "exact_consts.inc")).read()
+    c36 = _inc_table(text, "kXC36", (18, 18))
+    cols = list(range(9)) + list(range(18, 27))
+    assert np.array_equal(c36.view(np.uint32), tabs["cos36"][:, cols].astype(np.float32).view(np.uint32))
+    c12 = _inc_table(text, "kXC12", (6, 12))
+    assert np.array_equal(c12.view(np.uint32), tabs["cos12"].astype(np.float32).view(np.uint32))
+    nrow = _inc_table(text, "kXNrow", (33, 32))
+    n = tabs["synth_nwin"].astype(np.float32)
+    want = np.stack([n[m - 16] if m >= 16 else -n[48 - m] for m in range(32)] + [n[16]])
+    assert np.array_equal(nrow.view(np.uint32), want.view(np.uint32))
