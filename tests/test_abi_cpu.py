@@ -134,6 +134,9 @@ def test_exact_kernel_has_no_fma():
     assert all(re.search(r"\bv_(pk_)?fmac?_f32", b) for _, b in fast), "fast kernel lost its FMAs"
     for name, body in exact:
         assert "v_mul_f32" in body and "v_add_f32" in body, name
+        # (a v_fma_mix* with a zero addend is a product converted to f16: the
+        # band exponents n4 / 4, exact in both formats -- not a contraction)
+        body = re.sub(r"v_fma_mix\w+ [^\n]*, 0\n", "\n", body)
         bad = re.findall(r"\b(v_fma\w*|v_fmac\w*|v_mac_\w*|v_mad_\w*f32|v_pk_fma\w*)\b", body)
         assert not bad, (name, sorted(set(bad)))
 
