@@ -138,8 +138,10 @@ def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle, pip
     plan = mp3g.Plan(s["streams"], mode=mode, device=idx)
     h = stream.cuda_stream
 
+    # rows to count1 only: what the default plan kernels read (the batch and
+    # decoder APIs do the same, include/mp3g.h MP3G_HUFF_ROWS_COUNT1)
     def huff():
-        mp3g.huffman_execute(d_j, n, d_m, d_g, d_c, stream=h, device=idx)
+        mp3g.huffman_execute(d_j, n, d_m, d_g, d_c, stream=h, device=idx, flags=mp3g.HUFF_ROWS_COUNT1)
 
     for _ in range(warmup):
         huff()

@@ -94,6 +94,14 @@ __device__ __forceinline__ int kPretab(int sfb) { return (int)((0x2fe95400000ull
 //  * 2 x 32 x 34 x 4 = 8,704 B per wave, which with the raw coefficients in
 //    registers (no LDS copy) brings an 8-wave workgroup to 75 KB: 2
 //    workgroups = 16 waves per CU.
+// Coefficient prefetch bounded by count1 (lines at and above it are zero by
+// the parse's guarantee and need not be read, nor written by the Huffman
+// kernel): 2 = the next granule's descriptor staged in LDS one granule ahead
+// (c3 -0.4 %, tools/gpu_r03z.sh), 1 = its count1s by scalar loads (+1-2.5 %),
+// 0 = whole rows.
+#ifndef MP3G_FAST_SKIP_ZERO
+#define MP3G_FAST_SKIP_ZERO 2
+#endif
 constexpr int kHist = 16;
 // 16 waves per CU: <= 128 VGPRs (MI355X_MICROARCH.md register
 // table) next to the 40.5 KB of LDS per workgroup
@@ -133,6 +141,9 @@ struct __align__(16) WaveSmem {
   // of short-block granules (reorder gather) and the intensity-stereo pass
   float ring[2][32][kSlots];
   mp3g_granule desc;  // 16-B aligned: the channels' first 8 bytes are one 8-B read each
+#if MP3G_FAST_SKIP_ZERO == 2
+  mp3g_granule descn;  // the next granule's descriptor (its count1s bound its prefetch)
+#endif
   // requantization exponents n4 / 4 (float16, exact) of the long bands
   // [ch][sfb] and short bands [ch][sfb][win]
   _Float16 expo[2 * 22 + 2 * 39];
@@ -183,9 +194,6 @@ __device__ __forceinline__ void load_lines_lim(const int16_t* coef, uint32_t g, 
     cw[3 * i + 2] = v[2];
   }
 }
-#ifndef MP3G_FAST_SKIP_ZERO
-#define MP3G_FAST_SKIP_ZERO 0
-#endif
 // the line limit of lane (ch, sb) in granule g (wave-uniform g: scalar loads)
 __device__ __forceinline__ int count1_lim(const mp3g_granule* gran, uint32_t g, int lane) {
   const uint32_t h = gran[g].header;
@@ -1047,6 +1055,10 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
   if (w < end) {
     load_lines_lim(coef, w, lane, cw, (int)(MP3G_COEF_PER_GRANULE * sizeof(int16_t)), count1_lim(gran, w, lane));
     if (lane < 10) reinterpret_cast<uint4*>(&s.desc)[lane] = reinterpret_cast<const uint4*>(gran + w)[lane];
+#if MP3G_FAST_SKIP_ZERO == 2
+    if (lane < 10 && w + 1 < end)
+      reinterpret_cast<uint4*>(&s.descn)[lane] = reinterpret_cast<const uint4*>(gran + w + 1)[lane];
+#endif
   }
   wave_sync();
 
@@ -1075,7 +1087,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       else __builtin_amdgcn_s_setprio(0);
     }
     const bool out = g >= out_first;
-#if MP3G_FAST_SKIP_ZERO
+#if MP3G_FAST_SKIP_ZERO == 1
     // the next granule's channel count and count1s for its prefetch: scalar
     // loads issued here, long before the prefetch below needs them
     const uint32_t gq = g + 1 < end ? g + 1 : g;
@@ -1384,15 +1396,34 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     // issued unconditionally (straight-line vmcnt accounting, as the PCM
     // stores below): past the chunk the resources have no records
     {
-#if MP3G_FAST_SKIP_ZERO
+#if MP3G_FAST_SKIP_ZERO == 1
       const int lim = ch ? (hdr_nch(nx_h) == 2 ? (int)nx_c1 : 0) : (int)nx_c0;
       load_lines_lim(coef, g + 1, lane, cw, more ? (int)(MP3G_COEF_PER_GRANULE * sizeof(int16_t)) : 0, lim);
+#elif MP3G_FAST_SKIP_ZERO == 2
+      // the next granule's descriptor is already in LDS (loaded one granule
+      // earlier): its count1s bound this prefetch; the descriptor two ahead
+      // is loaded with it
+      {
+        const uint32_t nh = __builtin_amdgcn_readfirstlane(s.descn.header);
+        const uint2 n0 = *reinterpret_cast<const uint2*>(&s.descn.ch[0]);
+        const uint2 n1 = *reinterpret_cast<const uint2*>(&s.descn.ch[1]);
+        const int c0 = (int)(__builtin_amdgcn_readfirstlane(n0.x) & 0xffffu);
+        const int c1 = (int)(__builtin_amdgcn_readfirstlane(n1.x) & 0xffffu);
+        const int lim = ch ? (hdr_nch(nh) == 2 ? c1 : 0) : c0;
+        load_lines_lim(coef, g + 1, lane, cw, more ? (int)(MP3G_COEF_PER_GRANULE * sizeof(int16_t)) : 0, lim);
+      }
 #else
       load_lines(coef, g + 1, lane, cw, more ? (int)(MP3G_COEF_PER_GRANULE * sizeof(int16_t)) : 0);
 #endif
       if (lane < 10) {
+#if MP3G_FAST_SKIP_ZERO == 2
+        const bool more2 = g + 2 < end;
+        const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<mp3g_granule*>(gran + g + 2), (short)0, more2 ? (int)sizeof(mp3g_granule) : 0, 0x00020000);
+#else
         const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<mp3g_granule*>(gran + g + 1), (short)0, more ? (int)sizeof(mp3g_granule) : 0, 0x00020000);
+#endif
         const auto v = __builtin_amdgcn_raw_buffer_load_b128(rd, lane * 16, 0, 0);
         pd = make_uint4(v[0], v[1], v[2], v[3]);
       }
@@ -1435,7 +1466,14 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     //      before the PCM stores are issued -- vmcnt counts loads and stores in
     //      issue order, so a wait for the prefetch after the stores would wait
     //      for the stores too ----
+#if MP3G_FAST_SKIP_ZERO == 2
+    if (more && lane < 10) {
+      reinterpret_cast<uint4*>(&s.desc)[lane] = reinterpret_cast<const uint4*>(&s.descn)[lane];
+      reinterpret_cast<uint4*>(&s.descn)[lane] = pd;
+    }
+#else
     if (more && lane < 10) reinterpret_cast<uint4*>(&s.desc)[lane] = pd;
+#endif
 
     // ---- 16-tap window over the X ring -> s16 PCM, stored straight to HBM ----
     // (lanes of an absent channel compute values that are never stored)

@@ -50,6 +50,7 @@ struct __align__(16) XSharedSmem {
 struct __align__(16) XWaveSmem {
   float ring[2][kCols][kSlots];
   mp3g_granule desc;
+  mp3g_granule descn;  // the next granule's descriptor (its count1s bound its prefetch)
   _Float16 expo[2 * 22 + 2 * 39];
 };
 
@@ -265,8 +266,10 @@ granule_wexact_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, c
 
   uint32_t cw[9] = {};
   if (w < end) {
-    load_lines(coef, w, lane, cw);
+    load_lines_lim(coef, w, lane, cw, (int)(MP3G_COEF_PER_GRANULE * sizeof(int16_t)), count1_lim(gran, w, lane));
     if (lane < 10) reinterpret_cast<uint4*>(&s.desc)[lane] = reinterpret_cast<const uint4*>(gran + w)[lane];
+    if (lane < 10 && w + 1 < end)
+      reinterpret_cast<uint4*>(&s.descn)[lane] = reinterpret_cast<const uint4*>(gran + w + 1)[lane];
   }
   wave_sync();
   const uint32_t span = end - w, span2 = 2 * span, span3 = 3 * span;
@@ -299,10 +302,23 @@ granule_wexact_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, c
     const bool more = g + 1 < end;
     uint4 pd = {0, 0, 0, 0};
     {
-      load_lines(coef, g + 1, lane, cw, more ? (int)(MP3G_COEF_PER_GRANULE * sizeof(int16_t)) : 0);
+      // lines below the next granule's count1s only (its descriptor is in
+      // LDS since the previous granule; lines at and above count1 are zero,
+      // maindata/huffman.go:127-134, and need not be written by the Huffman
+      // kernel), the descriptor two granules ahead with them
+      {
+        const uint32_t nh = __builtin_amdgcn_readfirstlane(s.descn.header);
+        const uint2 n0 = *reinterpret_cast<const uint2*>(&s.descn.ch[0]);
+        const uint2 n1 = *reinterpret_cast<const uint2*>(&s.descn.ch[1]);
+        const int c0 = (int)(__builtin_amdgcn_readfirstlane(n0.x) & 0xffffu);
+        const int c1 = (int)(__builtin_amdgcn_readfirstlane(n1.x) & 0xffffu);
+        const int lim = lane_fresh() >> 5 ? (hdr_nch(nh) == 2 ? c1 : 0) : c0;
+        load_lines_lim(coef, g + 1, lane, cw, more ? (int)(MP3G_COEF_PER_GRANULE * sizeof(int16_t)) : 0, lim);
+      }
       if (lane < 10) {
+        const bool more2 = g + 2 < end;
         const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<mp3g_granule*>(gran + g + 1), (short)0, more ? (int)sizeof(mp3g_granule) : 0, 0x00020000);
+            const_cast<mp3g_granule*>(gran + g + 2), (short)0, more2 ? (int)sizeof(mp3g_granule) : 0, 0x00020000);
         const auto v = __builtin_amdgcn_raw_buffer_load_b128(rd, lane * 16, 0, 0);
         pd = make_uint4(v[0], v[1], v[2], v[3]);
       }
@@ -315,7 +331,10 @@ granule_wexact_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, c
     wave_sync();
     if (need_v && act && (lane & 31) < 18) matrix_exact_v16(&s.ring[ch][0][kHist + (lane & 31)]);
     wave_sync();
-    if (more && lane < 10) reinterpret_cast<uint4*>(&s.desc)[lane] = pd;
+    if (more && lane < 10) {
+      reinterpret_cast<uint4*>(&s.desc)[lane] = reinterpret_cast<const uint4*>(&s.descn)[lane];
+      reinterpret_cast<uint4*>(&s.descn)[lane] = pd;
+    }
 
     // ---- window -> s16 PCM (frame.go:649-678) ----
     uint32_t pk[9] = {};  // (replayed granules: stored to no records)

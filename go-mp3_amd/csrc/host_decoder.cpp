@@ -488,7 +488,8 @@ struct mp3g_decoder {
         e = hipMemcpyAsync(d_md, si + b_jobs, b.md.size(), hipMemcpyHostToDevice, stream);
       if (e == hipSuccess) e = hipMemcpyAsync(d_jobs, si, b_jobs, hipMemcpyHostToDevice, stream);
       if (e == hipSuccess) {
-        rc = mp3g_huffman_execute(device, d_jobs, n, d_md, d_gran, d_coef, stream);
+        rc = mp3g_huffman_execute_ex(device, d_jobs, n, d_md, d_gran, d_coef,
+                                     mode_reads_to_count1(mode) ? MP3G_HUFF_ROWS_COUNT1 : 0u, stream);
         if (rc) return rc;
       }
     } else if (e == hipSuccess) {

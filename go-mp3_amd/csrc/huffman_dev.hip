@@ -40,9 +40,6 @@ __device__ __forceinline__ uint64_t wave_max(uint64_t v) {
   return v;
 }
 
-#ifndef MP3G_HUFF_SHORT_ROWS
-#define MP3G_HUFF_SHORT_ROWS 0
-#endif
 // Block-sorted kernel: the 256 jobs of a block are ranked by big_values
 // (counting sort in LDS, bins of 4 pairs) before they are dealt to lanes, so
 // each wave's 64 lanes run big-values loops of similar length (the loop of a
@@ -66,7 +63,7 @@ constexpr int kBins = 128;  // bin 0: jobs that read nothing; 1 + big_values / 4
 #define MP3G_HUFF_SORTED_ATTR __attribute__((amdgpu_num_vgpr(MP3G_HUFF_MAXVGPR)))
 __global__ void __launch_bounds__(kThreads) MP3G_HUFF_SORTED_ATTR
 huffman_sorted_kernel(const mp3g_hjob* __restrict__ jobs, uint64_t n_jobs, const uint8_t* __restrict__ md,
-                      mp3g_granule* __restrict__ gran, int16_t* __restrict__ coef) {
+                      mp3g_granule* __restrict__ gran, int16_t* __restrict__ coef, uint32_t full_rows) {
   static_assert(kThreads <= 1024 && kThreads % 64 == 0, "block shape");
   __shared__ uint32_t T2[kHuffMaxEntries / 2];
   __shared__ uint32_t s_root[34], s_lin[34];
@@ -144,12 +141,14 @@ huffman_sorted_kernel(const mp3g_hjob* __restrict__ jobs, uint64_t n_jobs, const
       z = decode_job_direct(J, j, md, gran, coef, T, s_root, s_lin);
     }
   }
-#if MP3G_HUFF_SHORT_ROWS
-  // rows read only below count1 (rounded up to 6 lines) by the DSP: one 16-B
-  // slot of zeros past the lane's last block covers that
-  if (z < MP3G_LINES) *reinterpret_cast<uint4*>(coef + j * MP3G_LINES + z) = make_uint4(0u, 0u, 0u, 0u);
-  return;
-#endif
+  if (!full_rows) {
+    // rows to count1 only (MP3G_HUFF_ROWS_COUNT1): the default plan kernels
+    // read lines below count1 in 6-line pieces, i.e. up to count1 + 5 <= z + 5
+    // (z >= count1 is the end of the lane's last 16-line block): one 16-B slot
+    // of zeros past it covers that.  c3: 2.79 -> 2.42 ms (tools/gpu_r03z.sh)
+    if (z < MP3G_LINES) *reinterpret_cast<uint4*>(coef + j * MP3G_LINES + z) = make_uint4(0u, 0u, 0u, 0u);
+    return;
+  }
   // zero tails of the wave's 64 rows, one row at a time with the whole wave
   for (int rr = 0; rr < 64; rr++) {
     const int zr = __shfl(z, rr, 64);
@@ -163,11 +162,12 @@ huffman_sorted_kernel(const mp3g_hjob* __restrict__ jobs, uint64_t n_jobs, const
 }  // namespace huff
 
 hipError_t launch_huffman(const mp3g_hjob* d_jobs, uint64_t n_jobs, const uint8_t* d_md, mp3g_granule* d_gran,
-                          int16_t* d_coef, hipStream_t stream) {
+                          int16_t* d_coef, bool full_rows, hipStream_t stream) {
   if (n_jobs == 0) return hipSuccess;
   const uint64_t blocks = (n_jobs + huff::kThreads - 1) / huff::kThreads;
   hipLaunchKernelGGL(huff::huffman_sorted_kernel, dim3((uint32_t)blocks),
-                     dim3(huff::kThreads), 0, stream, d_jobs, n_jobs, d_md, d_gran, d_coef);
+                     dim3(huff::kThreads), 0, stream, d_jobs, n_jobs, d_md, d_gran, d_coef,
+                     full_rows ? 1u : 0u);
   return hipGetLastError();
 }
 

@@ -46,8 +46,10 @@ hipError_t launch_granule(int variant, const ChunkDesc* d_chunks, uint32_t n_chu
 int chunks_per_cu(int variant);
 
 // Main-data decode (huffman_dev.hip): one lane per (granule, channel) job.
+// full_rows = false: rows written only up to count1 (+ padding), enough for
+// the one-wave plan kernels (fast v3, exact v4) -- MP3G_HUFF_ROWS_COUNT1.
 hipError_t launch_huffman(const mp3g_hjob* d_jobs, uint64_t n_jobs, const uint8_t* d_md, mp3g_granule* d_gran,
-                          int16_t* d_coef, hipStream_t stream);
+                          int16_t* d_coef, bool full_rows, hipStream_t stream);
 
 // Diagnostic: fast kernel with per-phase s_memtime sums (8 per chunk) in d_stamps.
 constexpr int kFastPhases = 8;

@@ -100,6 +100,15 @@ int plan_variant(uint32_t mode) {
   return kVariantExact4;
 }
 
+}  // namespace
+
+bool mp3g::mode_reads_to_count1(unsigned mode) {
+  const int v = plan_variant(mode);
+  return v == kVariantFast || v == kVariantExact4;
+}
+
+namespace {
+
 uint32_t auto_chunk(const mp3g_stream* streams, uint32_t n_streams, int device, uint32_t mode) {
   uint64_t maxn = 0;
   for (uint32_t s = 0; s < n_streams; s++) maxn = std::max<uint64_t>(maxn, streams[s].n_granules);
@@ -390,13 +399,20 @@ int mp3g_plan_synth_execute(mp3g_plan* p, const mp3g_granule* d_gran, const floa
 
 int mp3g_huffman_execute(int device, const mp3g_hjob* d_jobs, uint64_t n_granules, const uint8_t* d_md,
                          mp3g_granule* d_gran, int16_t* d_coef, void* hip_stream) {
+  return mp3g_huffman_execute_ex(device, d_jobs, n_granules, d_md, d_gran, d_coef, 0u, hip_stream);
+}
+
+int mp3g_huffman_execute_ex(int device, const mp3g_hjob* d_jobs, uint64_t n_granules, const uint8_t* d_md,
+                            mp3g_granule* d_gran, int16_t* d_coef, uint32_t flags, void* hip_stream) {
+  if (flags & ~(uint32_t)MP3G_HUFF_ROWS_COUNT1) return fail(MP3G_ERR_INVALID_ARGUMENT, "huffman flags");
   if (n_granules == 0) return MP3G_OK;
   if (!d_jobs || !d_md || !d_gran || !d_coef) return fail(MP3G_ERR_INVALID_ARGUMENT, "null device buffer");
   DeviceGuard guard(device);
   if (guard.err != hipSuccess) return fail(MP3G_ERR_NO_DEVICE, "hipSetDevice", guard.err);
   int st = ensure_device(device);
   if (st) return st;
-  HIP_TRY(launch_huffman(d_jobs, 2 * n_granules, d_md, d_gran, d_coef, static_cast<hipStream_t>(hip_stream)));
+  HIP_TRY(launch_huffman(d_jobs, 2 * n_granules, d_md, d_gran, d_coef, !(flags & MP3G_HUFF_ROWS_COUNT1),
+                         static_cast<hipStream_t>(hip_stream)));
   return MP3G_OK;
 }
 

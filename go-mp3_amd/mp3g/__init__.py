@@ -16,7 +16,7 @@ import numpy as np
 __all__ = ["CHANNEL_DTYPE", "GRANULE_DTYPE", "STREAM_DTYPE", "STATE_DTYPE", "MODE_EXACT",
            "MODE_FAST", "FLAG_CHECKED", "FLAG_KERNEL_V1", "FLAG_KERNEL_V2", "FLAG_HOST_HUFFMAN", "STATE_IN", "STATE_OUT", "Mp3gError", "lib", "lib_path",
            "decode_host", "validate", "Plan", "device_count", "streams_for", "parse_stream",
-           "parse_streams", "Decoder", "HJOB_DTYPE", "scan_streams", "huffman_execute", "decode_streams"]
+           "parse_streams", "Decoder", "HJOB_DTYPE", "scan_streams", "huffman_execute", "HUFF_ROWS_COUNT1", "decode_streams"]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 
@@ -103,6 +103,7 @@ def lib():
         L.mp3g_lame_toc_offset.argtypes = [C.POINTER(_LameInfo), C.c_double, u64, C.POINTER(u64)]
         L.mp3g_lame_toc_offset.restype = C.c_int
         L.mp3g_huffman_execute.argtypes = [C.c_int, vp, u64, vp, vp, vp, vp]
+        L.mp3g_huffman_execute_ex.argtypes = [C.c_int, vp, u64, vp, vp, vp, u32, vp]
         L.mp3g_decode_streams.argtypes = [C.c_int, u32, vp, vp, C.c_int, u32, C.POINTER(vp), C.POINTER(u64),
                                           vp, vp]
         L.mp3g_decode_streams_into.argtypes = [C.c_int, u32, vp, vp, C.c_int, u32, u32, vp, u64, C.POINTER(u64),
@@ -259,13 +260,23 @@ def scan_streams(datas, n_threads=0):
         lib().mp3g_scan_free(h)
 
 
-def huffman_execute(d_jobs, n_granules, d_main_data, d_granules, d_coeffs, stream=None, device=0):
-    """Device scale-factor + Huffman decode of 2 * n_granules jobs (mp3g_huffman_execute);
-    buffers are device pointers (ints) or torch tensors, stream a hipStream_t int."""
+HUFF_ROWS_COUNT1 = 1  # mp3g_huffman_execute_ex: rows written only up to count1 (+ padding)
+
+
+def huffman_execute(d_jobs, n_granules, d_main_data, d_granules, d_coeffs, stream=None, device=0, flags=0):
+    """Device scale-factor + Huffman decode of 2 * n_granules jobs (mp3g_huffman_execute,
+    or mp3g_huffman_execute_ex with flags, e.g. HUFF_ROWS_COUNT1 when the rows feed a
+    default-kernel plan); buffers are device pointers (ints) or torch tensors, stream a
+    hipStream_t int."""
     def p(x):
         return C.c_void_p(x.data_ptr() if hasattr(x, "data_ptr") else int(x))
-    _check(lib().mp3g_huffman_execute(device, p(d_jobs), n_granules, p(d_main_data), p(d_granules),
-                                      p(d_coeffs), C.c_void_p(stream) if stream else None))
+    st = C.c_void_p(stream) if stream else None
+    if flags:
+        _check(lib().mp3g_huffman_execute_ex(device, p(d_jobs), n_granules, p(d_main_data), p(d_granules),
+                                             p(d_coeffs), flags, st))
+    else:
+        _check(lib().mp3g_huffman_execute(device, p(d_jobs), n_granules, p(d_main_data), p(d_granules),
+                                          p(d_coeffs), st))
 
 
 class _LameInfo(C.Structure):

@@ -126,7 +126,7 @@ typedef struct mp3g_stream {
 
 /* ---- decode modes -------------------------------------------------------- */
 #define MP3G_MODE_EXACT 0u   /* bit-exact vs the reference (linux/amd64 float semantics) */
-#define MP3G_MODE_FAST  1u   /* MFMA/fast-transform polyphase; |dPCM| <= 1 LSB          */
+#define MP3G_MODE_FAST  1u   /* reassociated fast transforms; |dPCM| <= 1 LSB            */
 #define MP3G_FLAG_CHECKED 0x100u /* validate descriptor ranges on the host first      */
 #define MP3G_FLAG_KERNEL_V1 0x200u /* exact mode via the per-phase v1 kernel (cross-check) */
 #define MP3G_FLAG_KERNEL_V2 0x800u /* exact mode via the workgroup v2 kernel (cross-check; the
@@ -282,6 +282,15 @@ void mp3g_scan_free(mp3g_scan* scan);
  * hip_stream (NULL = default stream). */
 int mp3g_huffman_execute(int device, const mp3g_hjob* d_jobs, uint64_t n_granules, const uint8_t* d_main_data,
                          mp3g_granule* d_granules, int16_t* d_coeffs, void* hip_stream);
+/* The same with flags.  MP3G_HUFF_ROWS_COUNT1: each coefficient row is
+ * written only up to its count1 plus padding (the zero tail is left as it
+ * was): what the default plan kernels (MP3G_MODE_FAST, and MP3G_MODE_EXACT
+ * without MP3G_FLAG_KERNEL_V1 / _V2) read, since lines at and above count1
+ * are zero (maindata/huffman.go:127-134).  The batch and decoder APIs use it
+ * for those modes (c3 main-data kernel -13 %). */
+#define MP3G_HUFF_ROWS_COUNT1 1u
+int mp3g_huffman_execute_ex(int device, const mp3g_hjob* d_jobs, uint64_t n_granules, const uint8_t* d_main_data,
+                            mp3g_granule* d_granules, int16_t* d_coeffs, uint32_t flags, void* hip_stream);
 
 /* Bitstreams in, PCM out (the batch drop-in): scan on the host, Huffman + DSP
  * on `device`.  *pcm (library-allocated, free with mp3g_free) holds

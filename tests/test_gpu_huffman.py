@@ -153,3 +153,45 @@ def test_decode_streams_into_pipelined(gpu, sample_files, n_groups):
         hi = int(s[k + 1]["first_granule"]) if k + 1 < len(datas) else n
         assert not pcm[lo + m:hi].any(), k  # the unused rest of an early-ended stream's range
     assert st[8] == 8 and 0 < s[8]["n_granules"] < s[9]["n_granules"]
+
+
+def test_rows_to_count1(gpu, sample_files):
+    """MP3G_HUFF_ROWS_COUNT1 (mp3g_huffman_execute_ex): over a poisoned buffer
+    each row equals the full-row decode up to its count1 + 5 lines (the
+    6-line pieces the default plan kernels read, rounded within the padding),
+    and those kernels (fast v3, exact v4) decode it to the same PCM as the
+    full rows; the tail past the padding is left untouched."""
+    import torch
+    from mp3g import synth
+    dev = torch.device("cuda:0")
+    datas = [sample_files["classic_lame.mp3"], sample_files["mpeg2.mp3"]]
+    datas += [synth.encode_stream(31 + k, 60, p_mixed=0.3, p_event=0.1, p_is=0.3) for k in range(4)]
+    s = gpu.scan_streams(datas, n_threads=4)
+    n = len(s["granules"])
+    st = torch.cuda.current_stream(dev).cuda_stream
+    outs = []
+    for flags in (0, gpu.HUFF_ROWS_COUNT1):
+        d_g = torch.from_numpy(s["granules"].view(np.uint8).copy()).to(dev)
+        d_j = torch.from_numpy(s["jobs"].view(np.uint8).copy()).to(dev)
+        d_m = torch.from_numpy(s["main_data"].copy()).to(dev)
+        d_c = torch.full((n * 1152,), 0x5A5A, dtype=torch.int16, device=dev)
+        gpu.huffman_execute(d_j, n, d_m, d_g, d_c, stream=st, flags=flags)
+        pcm = {}
+        for mode in (gpu.MODE_EXACT, gpu.MODE_FAST):
+            d_p = torch.zeros(n * 1152, dtype=torch.int16, device=dev)
+            plan = gpu.Plan(s["streams"], mode=mode)
+            plan.execute(d_g, d_c, d_p, stream=st)
+            torch.cuda.synchronize(dev)
+            plan.close()
+            pcm[mode] = d_p.cpu().numpy()
+        g = d_g.cpu().numpy().view(gpu.GRANULE_DTYPE)
+        outs.append((g, d_c.cpu().numpy().reshape(n, 2, 576), pcm))
+    (g0, c0, p0), (g1, c1, p1) = outs
+    assert g0.tobytes() == g1.tobytes()
+    lim = np.minimum(g0["ch"]["count1"].astype(np.int64) + 6, 576)  # [n][2]
+    line = np.arange(576)[None, None, :]
+    inside = line < lim[:, :, None]
+    assert np.array_equal(c1[inside], c0[inside])
+    assert (c1 == 0x5A5A).any(), "the tails should be left unwritten"
+    for mode in p0:
+        assert np.array_equal(p0[mode], p1[mode]), mode
