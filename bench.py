@@ -159,6 +159,10 @@ def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle, pip
     torch.cuda.synchronize(dev)
     huff_ms = ev[0].elapsed_time(ev[1]) / steps
     both_ms = ev[1].elapsed_time(ev[2]) / steps
+    # coefficient bytes the main-data kernel writes with MP3G_HUFF_ROWS_COUNT1:
+    # each row up to its count1 (the rest is the zero tail it skips)
+    c1 = d_g.cpu().numpy().view(mp3g.GRANULE_DTYPE)["ch"]["count1"].astype(np.int64)
+    coef_bytes = int(2 * c1.sum())
     # once more with PCIe: bitstream-derived buffers from pinned host memory
     # up, Huffman + DSP, PCM down (the host scan is timed separately above)
     hg = torch.from_numpy(s["granules"].view(np.uint8).copy()).pin_memory()
@@ -231,9 +235,12 @@ def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle, pip
            "huffman_plus_dsp_ms": round(both_ms, 4), "huffman_kernel_ms": round(huff_ms, 4),
            "huffman_frames_per_s": round(frames / (huff_ms * 1e-3), 1),
            # Huffman kernel algorithmic bytes: main data + 2 x 48-B jobs in;
-           # 2 x 1152 B coefficients + 2 x 63 B scale factors / count1 out per granule
-           "huffman_algorithmic_bytes_per_launch": md + n * (96 + 2304 + 126),
-           "huffman_algorithmic_gbps": round((md + n * (96 + 2304 + 126)) / (huff_ms * 1e-3) / 1e9, 2),
+           # the coefficient lines below count1 (MP3G_HUFF_ROWS_COUNT1; full rows
+           # would be 2 x 1152 B) + 2 x 63 B scale factors / count1 out per granule
+           "huffman_rows": "to count1 (mp3g_huffman_execute_ex, MP3G_HUFF_ROWS_COUNT1)",
+           "huffman_coef_bytes_written": coef_bytes,
+           "huffman_algorithmic_bytes_per_launch": md + n * (96 + 126) + coef_bytes,
+           "huffman_algorithmic_gbps": round((md + n * (96 + 126) + coef_bytes) / (huff_ms * 1e-3) / 1e9, 2),
            "huffman_traffic_bytes_per_launch": profiled_traffic(cfg, "mp3g::huff::huffman_sorted_kernel")[0],
            "main_data_bytes": md, "bitstream_bytes": int(sum(len(d) for d in datas)),
            "host_scan_s": round(scan_s, 4), "host_scan_frames_per_s": round(frames / scan_s, 1),
