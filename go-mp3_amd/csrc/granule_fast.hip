@@ -262,6 +262,27 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// One ds_read_b64 of an LDS pair on an address register of its own.  The
+// load/store optimizer merges neighbouring 8-B reads of one base into
+// ds_read2_b64, which the LDS serves as 4 x 16 lanes on 32 banks: the window
+// reads 17 ring columns per channel, and on 32 banks two of them share a bank
+// pair (34 c mod 32 = 2c mod 32).  A single ds_read_b64 is served as 2 x 32
+// lanes on 64 banks, where all 32 columns are distinct (34 c mod 64).
+#ifndef MP3G_WIN_B64_ALONE
+#define MP3G_WIN_B64_ALONE 0  // 1: conflicts 465 -> 353 M cycles per c3 synth launch, time +1.3 % (tools/gpu_r03w.sh)
+#endif
+template <class T>
+__device__ __forceinline__ T lds_read_alone(const T* p) {
+#if MP3G_WIN_B64_ALONE
+  typedef const T __attribute__((address_space(3))) lT;
+  lT* q = (lT*)p;
+  asm volatile("" : "+v"(q));
+  return *q;
+#else
+  return *p;
+#endif
+}
+
 // Branch-free selects (v_bfi_b32 / v_cndmask): keeps the compiler from turning
 // a per-lane choice between two cheap values into exec-mask branches.
 __device__ __forceinline__ float self(bool c, float a, float b) {
@@ -1502,7 +1523,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       for (int p = 0; p < 9; p++) acc2[p] = bcast(0.0f);
 #pragma unroll
       for (int v = -14; v <= 16; v += 2) {
-        const f2 A = RA[(kHist + v) / 2];  // slots (16+v, 17+v): 8-B aligned
+        const f2 A = lds_read_alone(&RA[(kHist + v) / 2]);  // slots (16+v, 17+v): 8-B aligned
         const f2 B = {RB[kHist + v - 1], RB[kHist + v]};
 #pragma unroll
         for (int t = 0; t < 8; t++) {
