@@ -94,14 +94,6 @@ __device__ __forceinline__ int kPretab(int sfb) { return (int)((0x2fe95400000ull
 //  * 2 x 32 x 34 x 4 = 8,704 B per wave, which with the raw coefficients in
 //    registers (no LDS copy) brings an 8-wave workgroup to 75 KB: 2
 //    workgroups = 16 waves per CU.
-// Coefficient prefetch bounded by count1 (lines at and above it are zero by
-// the parse's guarantee and need not be read, nor written by the Huffman
-// kernel): 2 = the next granule's descriptor staged in LDS one granule ahead
-// (c3 -0.4 %, tools/gpu_r03z.sh), 1 = its count1s by scalar loads (+1-2.5 %),
-// 0 = whole rows.
-#ifndef MP3G_FAST_SKIP_ZERO
-#define MP3G_FAST_SKIP_ZERO 2
-#endif
 constexpr int kHist = 16;
 // 16 waves per CU: <= 128 VGPRs (MI355X_MICROARCH.md register
 // table) next to the 40.5 KB of LDS per workgroup
@@ -141,9 +133,12 @@ struct __align__(16) WaveSmem {
   // of short-block granules (reorder gather) and the intensity-stereo pass
   float ring[2][32][kSlots];
   mp3g_granule desc;  // 16-B aligned: the channels' first 8 bytes are one 8-B read each
-#if MP3G_FAST_SKIP_ZERO == 2
-  mp3g_granule descn;  // the next granule's descriptor (its count1s bound its prefetch)
-#endif
+  // the next granule's descriptor, one granule ahead: its count1s bound the
+  // next granule's coefficient prefetch (lines at and above count1 are zero by
+  // the parse's guarantee, maindata/huffman.go:127-134, so they are neither
+  // read here nor written by the main-data kernel, MP3G_HUFF_ROWS_COUNT1;
+  // c3 -0.4 % against whole rows, tools/gpu_r03z.sh)
+  mp3g_granule descn;
   // requantization exponents n4 / 4 (float16, exact) of the long bands
   // [ch][sfb] and short bands [ch][sfb][win]
   _Float16 expo[2 * 22 + 2 * 39];
@@ -260,27 +255,6 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// One ds_read_b64 of an LDS pair on an address register of its own.  The
-// load/store optimizer merges neighbouring 8-B reads of one base into
-// ds_read2_b64, which the LDS serves as 4 x 16 lanes on 32 banks: the window
-// reads 17 ring columns per channel, and on 32 banks two of them share a bank
-// pair (34 c mod 32 = 2c mod 32).  A single ds_read_b64 is served as 2 x 32
-// lanes on 64 banks, where all 32 columns are distinct (34 c mod 64).
-#ifndef MP3G_WIN_B64_ALONE
-#define MP3G_WIN_B64_ALONE 0  // 1: conflicts 465 -> 353 M cycles per c3 synth launch, time +1.3 % (tools/gpu_r03w.sh)
-#endif
-template <class T>
-__device__ __forceinline__ T lds_read_alone(const T* p) {
-#if MP3G_WIN_B64_ALONE
-  typedef const T __attribute__((address_space(3))) lT;
-  lT* q = (lT*)p;
-  asm volatile("" : "+v"(q));
-  return *q;
-#else
-  return *p;
-#endif
 }
 
 // Branch-free selects (v_bfi_b32 / v_cndmask): keeps the compiler from turning
@@ -1076,10 +1050,8 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
   if (w < end) {
     load_lines_lim(coef, w, lane, cw, (int)(MP3G_COEF_PER_GRANULE * sizeof(int16_t)), count1_lim(gran, w, lane));
     if (lane < 10) reinterpret_cast<uint4*>(&s.desc)[lane] = reinterpret_cast<const uint4*>(gran + w)[lane];
-#if MP3G_FAST_SKIP_ZERO == 2
     if (lane < 10 && w + 1 < end)
       reinterpret_cast<uint4*>(&s.descn)[lane] = reinterpret_cast<const uint4*>(gran + w + 1)[lane];
-#endif
   }
   wave_sync();
 
@@ -1108,13 +1080,6 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       else __builtin_amdgcn_s_setprio(0);
     }
     const bool out = g >= out_first;
-#if MP3G_FAST_SKIP_ZERO == 1
-    // the next granule's channel count and count1s for its prefetch: scalar
-    // loads issued here, long before the prefetch below needs them
-    const uint32_t gq = g + 1 < end ? g + 1 : g;
-    const uint32_t nx_h = gran[gq].header;
-    const uint32_t nx_c0 = gran[gq].ch[0].count1, nx_c1 = gran[gq].ch[1].count1;
-#endif
     // does a replayed granule's V feed anything? (see v2 / DESIGN.md halo)
     bool need_v = true;
     if (!out && g + 1 < out_first) need_v = hdr_nch(gran[g + 1].header) < hdr_nch(s.desc.header);
@@ -1417,10 +1382,6 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     // issued unconditionally (straight-line vmcnt accounting, as the PCM
     // stores below): past the chunk the resources have no records
     {
-#if MP3G_FAST_SKIP_ZERO == 1
-      const int lim = ch ? (hdr_nch(nx_h) == 2 ? (int)nx_c1 : 0) : (int)nx_c0;
-      load_lines_lim(coef, g + 1, lane, cw, more ? (int)(MP3G_COEF_PER_GRANULE * sizeof(int16_t)) : 0, lim);
-#elif MP3G_FAST_SKIP_ZERO == 2
       // the next granule's descriptor is already in LDS (loaded one granule
       // earlier): its count1s bound this prefetch; the descriptor two ahead
       // is loaded with it
@@ -1433,18 +1394,10 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
         const int lim = ch ? (hdr_nch(nh) == 2 ? c1 : 0) : c0;
         load_lines_lim(coef, g + 1, lane, cw, more ? (int)(MP3G_COEF_PER_GRANULE * sizeof(int16_t)) : 0, lim);
       }
-#else
-      load_lines(coef, g + 1, lane, cw, more ? (int)(MP3G_COEF_PER_GRANULE * sizeof(int16_t)) : 0);
-#endif
       if (lane < 10) {
-#if MP3G_FAST_SKIP_ZERO == 2
         const bool more2 = g + 2 < end;
         const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<mp3g_granule*>(gran + g + 2), (short)0, more2 ? (int)sizeof(mp3g_granule) : 0, 0x00020000);
-#else
-        const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<mp3g_granule*>(gran + g + 1), (short)0, more ? (int)sizeof(mp3g_granule) : 0, 0x00020000);
-#endif
         const auto v = __builtin_amdgcn_raw_buffer_load_b128(rd, lane * 16, 0, 0);
         pd = make_uint4(v[0], v[1], v[2], v[3]);
       }
@@ -1487,14 +1440,10 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     //      before the PCM stores are issued -- vmcnt counts loads and stores in
     //      issue order, so a wait for the prefetch after the stores would wait
     //      for the stores too ----
-#if MP3G_FAST_SKIP_ZERO == 2
     if (more && lane < 10) {
       reinterpret_cast<uint4*>(&s.desc)[lane] = reinterpret_cast<const uint4*>(&s.descn)[lane];
       reinterpret_cast<uint4*>(&s.descn)[lane] = pd;
     }
-#else
-    if (more && lane < 10) reinterpret_cast<uint4*>(&s.desc)[lane] = pd;
-#endif
 
     // ---- 16-tap window over the X ring -> s16 PCM, stored straight to HBM ----
     // (lanes of an absent channel compute values that are never stored)
@@ -1523,7 +1472,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       for (int p = 0; p < 9; p++) acc2[p] = bcast(0.0f);
 #pragma unroll
       for (int v = -14; v <= 16; v += 2) {
-        const f2 A = lds_read_alone(&RA[(kHist + v) / 2]);  // slots (16+v, 17+v): 8-B aligned
+        const f2 A = RA[(kHist + v) / 2];  // slots (16+v, 17+v): 8-B aligned
         const f2 B = {RB[kHist + v - 1], RB[kHist + v]};
 #pragma unroll
         for (int t = 0; t < 8; t++) {

@@ -255,7 +255,7 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
       for (int p = 0; p < 9; p++) acc2[p] = bcast(0.0f);
 #pragma unroll
       for (int v = -14; v <= 16; v += 2) {
-        const f2 Av = lds_read_alone(&RA[(kHist + v) / 2]);
+        const f2 Av = RA[(kHist + v) / 2];
         const f2 Bv = {RB[kHist + v - 1], RB[kHist + v]};
 #pragma unroll
         for (int t = 0; t < 8; t++) {

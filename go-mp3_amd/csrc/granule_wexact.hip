@@ -33,9 +33,6 @@ namespace v4 {
 using namespace v3;
 
 constexpr int kXWaves = 8;
-#ifndef MP3G_WEXACT_PK
-#define MP3G_WEXACT_PK 0  // 1: SGPR-pair constants hoisted and spilled (482 lane spills in the loop)
-#endif
 constexpr int kCols = 33;     // 32 X columns + V[16]
 constexpr int kColV16 = 32;
 
@@ -165,25 +162,6 @@ __device__ __forceinline__ void matrix_exact_v16(float* colu) {
 #pragma unroll
   for (int j = 0; j < 32; j++) S[j] = colu[kSlots * j];
   const float z0 = ozero();
-#if MP3G_WEXACT_PK
-  // rows (m, m + 1) as float pairs: v_pk_mul_f32 / v_pk_add_f32 round each
-  // element as the scalar forms do (two sums in one issue slot); V[16] alone
-  const f2 zz = (f2){z0, z0};
-#pragma unroll
-  for (int m = 0; m < 32; m += 2) {
-    f2 s = zz;
-#pragma unroll
-    for (int j = 0; j < 32; j++) s = s + (f2){kXNrow[m][j], kXNrow[m + 1][j]} * (f2){S[j], S[j]};
-    colu[kSlots * dct32::kPosOfM[m]] = s.x;
-    colu[kSlots * dct32::kPosOfM[m + 1]] = s.y;
-  }
-  {
-    float s = z0;
-#pragma unroll
-    for (int j = 0; j < 32; j++) s = s + kXNrow[32][j] * S[j];
-    colu[kSlots * kColV16] = s;
-  }
-#else
 #pragma unroll
   for (int m = 0; m < 33; m++) {
     float s = z0;
@@ -191,7 +169,6 @@ __device__ __forceinline__ void matrix_exact_v16(float* colu) {
     for (int j = 0; j < 32; j++) s = s + kXNrow[m][j] * S[j];
     colu[kSlots * (m < 32 ? dct32::kPosOfM[m] : kColV16)] = s;
   }
-#endif
 }
 
 // V[i] of the slot at x (the reference's value, bit for bit: 0 - x, not -x,
