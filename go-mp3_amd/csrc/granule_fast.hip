@@ -297,12 +297,14 @@ __device__ __forceinline__ int lane_fresh() {
 // X of a V block: X[m] = V[m-16] (m >= 16), -V[48-m] (m < 16).
 __device__ __forceinline__ float x_from_v(const float* v, int m) { return m >= 16 ? v[m - 16] : -v[48 - m]; }
 // V of an X vector (inverse identity; V[16] = 0).
-// x: one slot of the column-major ring (X[m] at x[kSlots * kPosOfM[m]]).
+// x: one slot of the column-major ring (X[m] at x[kS * kPosOfM[m]], kS the
+// ring's column stride).
+template <int kS = kSlots>
 __device__ __forceinline__ float v_from_x(const float* x, int i) {
-  if (i < 16) return x[kSlots * dct32::kPosOfM[16 + i]];
+  if (i < 16) return x[kS * dct32::kPosOfM[16 + i]];
   if (i == 16) return 0.0f;
-  if (i < 48) return -x[kSlots * dct32::kPosOfM[48 - i]];
-  return -x[kSlots * dct32::kPosOfM[i - 48]];
+  if (i < 48) return -x[kS * dct32::kPosOfM[48 - i]];
+  return -x[kS * dct32::kPosOfM[i - 48]];
 }
 
 // ---- reference-order fallback for hot granules ------------------------------
@@ -379,14 +381,16 @@ __device__ __forceinline__ cfloat4* stab(const float* p) {
   return q;
 }
 
-// The per-slot test on S in the ring's current slots (wave-uniform).
-__device__ __forceinline__ bool slot_sums_hot(const float (&ring)[2][32][kSlots], int nch) {
+// The per-slot test on S in the ring's current slots (wave-uniform); kS the
+// column stride, cur the first current slot.
+template <int kS = kSlots>
+__device__ __forceinline__ bool slot_sums_hot(const float (&ring)[2][32][kS], int nch, int cur = kHist) {
   const int lane = lane_fresh();
   const int c = lane >> 5, slot = lane & 31;
   float sum = 0.0f;
   if (c < nch && slot < 18) {
 #pragma unroll
-    for (int sb = 0; sb < 32; sb++) sum += fabsf(ring[c][sb][kHist + slot]);
+    for (int sb = 0; sb < 32; sb++) sum += fabsf(ring[c][sb][cur + slot]);
   }
   return __builtin_amdgcn_ballot_w64(sum > kHotL1) != 0;
 }
@@ -460,18 +464,19 @@ __device__ __forceinline__ void imdct_exact(const float x[18], int bt, int k, bo
 
 // V = synthNWin * S of one time slot in the reference's order
 // (frame.go:642-648), as its 32 distinct values X (in place in the ring
-// column slot `colu`: S[j] at colu[kSlots j], X[m] to colu[kSlots kPosOfM[m]]).
+// column slot `colu`: S[j] at colu[kS j], X[m] to colu[kS kPosOfM[m]]).
+template <int kS = kSlots>
 __device__ __forceinline__ void matrix_exact(float* colu) {
 #pragma clang fp contract(off)
   float S[32];
 #pragma unroll
-  for (int j = 0; j < 32; j++) S[j] = colu[kSlots * j];
+  for (int j = 0; j < 32; j++) S[j] = colu[kS * j];
   for (int m = 0; m < 32; m++) {
     const float* row = vtab(&g_fast.nrow[m][0]);
     float s = 0.0f;
 #pragma unroll
     for (int j = 0; j < 32; j++) s = s + row[j] * S[j];
-    colu[kSlots * dct32::kPosOfM[m]] = s;
+    colu[kS * dct32::kPosOfM[m]] = s;
   }
 }
 
@@ -481,6 +486,8 @@ __device__ __forceinline__ void matrix_exact(float* colu) {
 // window (RA / RB: the X columns of V_j[i], j even, and V_j[32 + i], j odd;
 // the V -> X signs are folded into FastTables::dwin, exactly).  V[16] (the
 // reference's ~1e-16 |S| residue of a zero row) is taken as 0.
+// (cur: the first current slot of the column layout, kHist in the fused kernel)
+template <int cur = kHist>
 __device__ __forceinline__ void window_exact(const float* RA, const float* RB, int k, f2 acc2[9]) {
 #pragma clang fp contract(off)
   float dw[16];
@@ -490,7 +497,7 @@ __device__ __forceinline__ void window_exact(const float* RA, const float* RB, i
   for (int ss = 0; ss < 18; ss++) {
     float sum = 0.0f;
 #pragma unroll
-    for (int j = 0; j < 16; j++) sum = sum + ((j & 1) ? RB : RA)[kHist + ss - j] * dw[j];
+    for (int j = 0; j < 16; j++) sum = sum + ((j & 1) ? RB : RA)[cur + ss - j] * dw[j];
     const float t = sum * 32767.0f;
     if (ss & 1) acc2[ss >> 1].y = t;
     else acc2[ss >> 1].x = t;

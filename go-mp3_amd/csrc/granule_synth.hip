@@ -40,8 +40,24 @@ constexpr int kSynthWaves = 8;
 #endif
 
 
+// Ping-pong ring: 36 slots per column, two halves of 18.  A granule's 18
+// slots go to one half while the other half holds the previous granule's,
+// whose last 15 are the history its window reads; the next granule writes the
+// half just read from.  No history shift (the fused kernel's 34-slot ring
+// moves 16 slots per column and granule; leaving that shift out of this
+// kernel measured -6 %, tools/gpu_synthlds.sh).  A window operand is named by
+// its virtual slot z = 16 + (V block - first block of the current granule),
+// z = 1..33, as in the fused kernel; physically
+//   even granules (P = 0): current in 18..35, history in 2..17: z + 2
+//   odd granules  (P = 1): current in 0..17, history in 20..35:
+//                          z - 16 (z >= 16) or z + 20
+// The hot-zone fixup (reference order, rare) keeps the even layout and moves
+// slots 20..35 to 2..17 after each granule.
+constexpr int kSS = 36;
+__device__ __forceinline__ constexpr int sphys(int P, int z) { return P ? (z >= 16 ? z - 16 : z + 20) : z + 2; }
+
 struct __align__(16) SynthWaveSmem {
-  float ring[2][32][kSlots];
+  float ring[2][32][kSS];
   uint32_t zone[kZones][2];  // hot zones of the chunk (record_hot)
 };
 
@@ -62,9 +78,10 @@ __device__ __forceinline__ void synth_load(const float* lines, uint32_t g, uint3
   }
 }
 
-// stage: line 18 sb + ss of channel c -> ring[c][sb][16 + ss], as 8-B pairs
-// (ds_write_b64, 4 x 16 lanes: as separate dwords the 32 lanes of a write
-// group land on 16 even banks)
+// stage: line 18 sb + ss of channel c -> ring[c][sb][cur + ss] (cur: the
+// first slot of the current half), as 8-B pairs (ds_write_b64, 4 x 16 lanes:
+// as separate dwords the 32 lanes of a write group land on 16 even banks)
+template <int cur>
 __device__ __forceinline__ void synth_stage(SynthWaveSmem& s, const f2 buf[9], int nch) {
 #pragma unroll
   for (int r = 0; r < 9; r++) {
@@ -73,7 +90,7 @@ __device__ __forceinline__ void synth_stage(SynthWaveSmem& s, const f2 buf[9], i
     const int l = e - 576 * c;
     const int sb = (l * 3641) >> 16;  // l / 18 for l < 576
     f2* colp = reinterpret_cast<f2*>(&s.ring[c][0][0]);
-    if (c < nch) colp[17 * sb + kHist / 2 + ((l - 18 * sb) >> 1)] = buf[r];
+    if (c < nch) colp[(kSS / 2) * sb + cur / 2 + ((l - 18 * sb) >> 1)] = buf[r];
   }
 }
 
@@ -104,14 +121,15 @@ __device__ __forceinline__ uint32_t synth_replay_start(const ChunkDesc& cd, uint
   return __builtin_amdgcn_readfirstlane((uint32_t)w64);
 }
 
-// V history of a replay start: X vectors from the stream's state_in or zero.
+// V history of a replay start (the even layout: block b at virtual slot
+// 15 - b): X vectors from the stream's state_in or zero.
 __device__ __forceinline__ void synth_init_ring(SynthWaveSmem& s, const mp3g_state* sin, const int init_in[2],
                                                 int lane) {
   const bool in0 = init_in[0] && sin, in1 = init_in[1] && sin;
   for (int e = lane; e < 2 * 15 * 32; e += kLanes) {
     const int c = e / (15 * 32), blk = (e >> 5) % 15, m = e & 31;
     const bool in = c ? in1 : in0;
-    s.ring[c][dct32::kPosOfM[m]][kHist - 1 - blk] = in ? x_from_v(&sin->vvec[c][64 * blk], m) : 0.0f;
+    s.ring[c][dct32::kPosOfM[m]][sphys(0, 15 - blk)] = in ? x_from_v(&sin->vvec[c][64 * blk], m) : 0.0f;
   }
 }
 
@@ -126,25 +144,25 @@ __device__ __forceinline__ bool synth_exact_granule(const mp3g_granule* __restri
   f2 buf[9];
   synth_load(lines, g, nch * 2304u, lane, buf);
   const bool hot1 = __builtin_amdgcn_ballot_w64(max_abs_pairs(buf) > kHotS) != 0;
-  synth_stage(s, buf, nch);
+  synth_stage<18>(s, buf, nch);
   wave_sync();
-  const bool hot = hot1 && slot_sums_hot(s.ring, nch);
-  if (ch < nch && (lane & 31) < 18) matrix_exact(&s.ring[ch][0][kHist + (lane & 31)]);
+  const bool hot = hot1 && slot_sums_hot<kSS>(s.ring, nch, 18);
+  if (ch < nch && (lane & 31) < 18) matrix_exact<kSS>(&s.ring[ch][0][18 + (lane & 31)]);
   wave_sync();
   uint32_t pk[9] = {};
   if (out) {
     const int pa = dct32::kPosOfM[k < 16 ? 16 + k : (k == 16 ? 0 : 48 - k)];
     const int pb = dct32::kPosOfM[k < 16 ? 16 - k : k - 16];
     f2 acc2[9];
-    window_exact(&s.ring[ch][pa][0], &s.ring[ch][pb][0], k, acc2);
+    window_exact<18>(&s.ring[ch][pa][0], &s.ring[ch][pb][0], k, acc2);
     pack_pcm(acc2, nch, pk);
   }
   store_pcm(pcm, g, out, pk, hi, k);
   wave_sync();
-  if (ch < nch) {
+  if (ch < nch) {  // slots 20..35 -> 2..17 (the even layout's history)
     f2* col = reinterpret_cast<f2*>(&s.ring[ch][k][0]);
 #pragma unroll
-    for (int q = 0; q < 8; q++) col[q] = col[9 + q];
+    for (int q = 0; q < 8; q++) col[1 + q] = col[10 + q];
   }
   wave_sync();
   return hot;
@@ -208,7 +226,13 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
   // -- two granules in flight, the taps read from LDS per granule to stay at
   // 116 VGPRs -- measured +1.5 % at c3: the loads are not latency-bound,
   // DESIGN.md "Standalone polyphase kernel")
-  auto step = [&](uint32_t g, f2 (&buf)[9], uint32_t gn) {
+  // one granule with the ring in layout P (std::integral_constant): stage buf
+  // (granule g), refill buf with granule gn, then the matrixing, window and
+  // PCM stores of g.  No history shift: the next granule uses the other
+  // layout, whose history half this granule's current half is.
+  auto step = [&](auto Pc, uint32_t g, f2 (&buf)[9], uint32_t gn) {
+    constexpr int P = decltype(Pc)::value;
+    constexpr int cur = P ? 0 : 18;  // first slot of the current half
     // progress-balanced issue priority, as in the fused kernel (c2 -3.5 %)
     const uint32_t left4 = 4u * (end - g);
     if (left4 > span3) __builtin_amdgcn_s_setprio(3);
@@ -221,32 +245,42 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
 #if MP3G_HOT_CHECK
     const bool hot1 = __builtin_amdgcn_ballot_w64(max_abs_pairs(buf) > kHotS) != 0;
 #endif
-    if (!(MP3G_SYNTH_ABL & 1)) synth_stage(s, buf, nch);
+    if (!(MP3G_SYNTH_ABL & 1)) synth_stage<cur>(s, buf, nch);
     // a later granule in flight during the matrixing and window
     load(gn, buf);
+    // a mono granule leaves channel 1 alone (Decode touches ch < nch): its
+    // history moves to the other layout's history half (lane (1, k): column k)
+    if (nch == 1 && ch == 1) {
+      f2* col = reinterpret_cast<f2*>(&s.ring[1][k][0]);
+#pragma unroll
+      for (int q = 0; q < 8; q++) col[P ? 1 + q : 10 + q] = col[P ? 10 + q : 1 + q];
+    }
     wave_sync();
 #if MP3G_HOT_CHECK
     // a hot granule (two tests, the second rare and on the staged S): its
     // zone is redone in the reference's order after the pass
-    if (hot1 && slot_sums_hot(s.ring, nch)) record_hot(s, nz, g, out_first, end);
+    if (hot1 && slot_sums_hot<kSS>(s.ring, nch, cur)) record_hot(s, nz, g, out_first, end);
 #endif
     // ---- matrixing (frame.go:642-648): lane (ch, slot) turns its S row into X ----
     {
       const int slot = lane & 31;
       if (!(MP3G_SYNTH_ABL & 2) && ch < nch && slot < 18) {
-        float* colu = &s.ring[ch][0][kHist + slot];
+        float* colu = &s.ring[ch][0][cur + slot];
         dct32::f2 sp[16];
 #pragma unroll
-        for (int q = 0; q < 16; q++) sp[q] = (dct32::f2){colu[kSlots * 2 * q], colu[kSlots * (2 * q + 1)]};
+        for (int q = 0; q < 16; q++) sp[q] = (dct32::f2){colu[kSS * 2 * q], colu[kSS * (2 * q + 1)]};
         dct32::dct2_32_to(sp, [&](int t, dct32::f2 v) {
-          colu[kSlots * dct32::kColX[t]] = v.x;
-          colu[kSlots * dct32::kColY[t]] = v.y;
+          colu[kSS * dct32::kColX[t]] = v.x;
+          colu[kSS * dct32::kColY[t]] = v.y;
         });
       }
     }
     wave_sync();
     // ---- 16-tap window -> s16 PCM (frame.go:649-678); the stores are issued
-    //      for replayed granules too, through a resource with no records ----
+    //      for replayed granules too, through a resource with no records.
+    //      Operands by virtual slot z (see SynthWaveSmem): A = the pair
+    //      (z, z + 1), z = 16 + v even (8-B aligned in both layouts), B = z - 1
+    //      and z (two dwords; in layout 1 the pair (15, 16) wraps) ----
     if (out && !(MP3G_SYNTH_ABL & 4)) {
       const f2* RA = reinterpret_cast<const f2*>(&s.ring[ch][pa][0]);
       const float* RB = &s.ring[ch][pb][0];
@@ -255,8 +289,8 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
       for (int p = 0; p < 9; p++) acc2[p] = bcast(0.0f);
 #pragma unroll
       for (int v = -14; v <= 16; v += 2) {
-        const f2 Av = RA[(kHist + v) / 2];
-        const f2 Bv = {RB[kHist + v - 1], RB[kHist + v]};
+        const f2 Av = RA[sphys(P, 16 + v) / 2];
+        const f2 Bv = {RB[sphys(P, 15 + v)], RB[sphys(P, 16 + v)]};
 #pragma unroll
         for (int t = 0; t < 8; t++) {
           const int p = v / 2 + t;
@@ -269,14 +303,7 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
       pack_pcm(acc2, nch, pk);
     }
     store_pcm(pcm, g, out, pk, hi, k);
-    wave_sync();
-    // ---- history shift of the channels this granule touched ----
-    if (!(MP3G_SYNTH_ABL & 8) && ch < nch) {
-      f2* col = reinterpret_cast<f2*>(&s.ring[ch][k][0]);
-#pragma unroll
-      for (int q = 0; q < 8; q++) col[q] = col[9 + q];
-    }
-    wave_sync();
+    wave_sync();  // window reads done before the next granule stages over them
   };
   // Loads are issued right after a granule is staged and waited for when it
   // is staged; the preheader pads each buffer's loads with nine stores to no
@@ -288,10 +315,16 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
   load(w, A);
   store_pcm(pcm, w, false, pk, hi, k);
   wave_sync();
-  for (uint32_t g = w; g < end; g++) step(g, A, g + 1);
+  // granules in pairs: layout 0, then layout 1 (scalar control)
+  for (uint32_t g = w; g < end; g += 2) {
+    step(std::integral_constant<int, 0>{}, g, A, g + 1);
+    if (g + 1 < end) step(std::integral_constant<int, 1>{}, g + 1, A, g + 2);
+  }
 
   // vVec out; the IMDCT overlap `store` is not this stage's: passed through
-  auto export_state = [&]() {
+  // (Pn: the layout the next granule would use, whose history half holds the
+  // last 15 V blocks)
+  auto export_state = [&](int Pn) {
     if (!(cd.flags & kChunkStateOut)) return;
     mp3g_state* so = state_out + cd.stream;
     const bool have_in = (cd.flags & kChunkStateIn) && sin;
@@ -299,10 +332,11 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
       (&so->store[0][0][0])[e] = have_in ? (&sin->store[0][0][0])[e] : 0.0f;
     for (int e = lane_fresh(); e < 2 * 1024; e += kLanes) {
       const int c = e >> 10, blk = (e >> 6) & 15, i = e & 63;
-      so->vvec[c][64 * blk + i] = blk < 15 ? v_from_x(&s.ring[c][0][kHist - 1 - blk], i) : 0.0f;
+      so->vvec[c][64 * blk + i] =
+          blk < 15 ? v_from_x<kSS>(&s.ring[c][0][Pn ? sphys(1, 15 - blk) : sphys(0, 15 - blk)], i) : 0.0f;
     }
   };
-  export_state();
+  export_state((int)((end - w) & 1u));
 
   // ---- hot zones (rare): redone in the reference's order from their replay
   //      start, PCM overwritten; a zone reaching the chunk end rewrites the
@@ -326,7 +360,7 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
         if (synth_exact_granule(gran, lines, pcm, s, g, g >= zs)) ze = g + 2 > ze ? (g + 2 < end ? g + 2 : end) : ze;
       done = g;
     }
-    if (done >= end) export_state();
+    if (done >= end) export_state(0);
   }
 }
 
