@@ -40,7 +40,7 @@ constexpr int kSynthWaves = 8;
 #endif
 
 
-// Ping-pong ring: 36 slots per column, two halves of 18.  A granule's 18
+// Ping-pong ring: 36 slots per column (stride 38), two halves of 18.  A granule's 18
 // slots go to one half while the other half holds the previous granule's,
 // whose last 15 are the history its window reads; the next granule writes the
 // half just read from.  No history shift (the fused kernel's 34-slot ring
@@ -53,7 +53,11 @@ constexpr int kSynthWaves = 8;
 //                          z - 16 (z >= 16) or z + 20
 // The hot-zone fixup (reference order, rare) keeps the even layout and moves
 // slots 20..35 to 2..17 after each granule.
-constexpr int kSS = 36;
+// column stride 38 (36 slots used): 38 = 6 mod 32 and 38 = 2 * 19 mod 64 map
+// the columns onto the banks exactly as the fused kernel's 34 does (column
+// mod 16 for dword reads, mod 32 for 8-B reads); a stride of 36 (4 mod 32)
+// folds them onto 8 bank groups (3.1 conflict cycles per LDS op at c3)
+constexpr int kSS = 38;
 __device__ __forceinline__ constexpr int sphys(int P, int z) { return P ? (z >= 16 ? z - 16 : z + 20) : z + 2; }
 
 struct __align__(16) SynthWaveSmem {
