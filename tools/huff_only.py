@@ -41,13 +41,14 @@ def main():
     d_m = torch.from_numpy(s["main_data"].copy()).to(dev)
     d_c = torch.empty(n * 1152, dtype=torch.int16, device=dev)
     st = torch.cuda.current_stream()
+    flags = mp3g.HUFF_ROWS_COUNT1 if os.environ.get("HUFF_ROWS", "1") == "1" else 0  # rows to count1 (default)
     for _ in range(2):
-        mp3g.huffman_execute(d_j, n, d_m, d_g, d_c, stream=st.cuda_stream, device=0)
+        mp3g.huffman_execute(d_j, n, d_m, d_g, d_c, stream=st.cuda_stream, device=0, flags=flags)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(st)
     for _ in range(iters):
-        mp3g.huffman_execute(d_j, n, d_m, d_g, d_c, stream=st.cuda_stream, device=0)
+        mp3g.huffman_execute(d_j, n, d_m, d_g, d_c, stream=st.cuda_stream, device=0, flags=flags)
     e1.record(st)
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / iters
