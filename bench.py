@@ -338,6 +338,22 @@ def polyphase_leg(args, rank, dev, stream, d_g, streams, n_gran, local):
 PROFILE_TAG = "r03c"  # profiles/<tag>_<cfg>_<kernel>.json of the current kernels
 
 
+def profiled_issue(cfg, kernel):
+    """VALU issue utilisation and LDS conflict cycles per LDS instruction of the
+    kernel in the newest profile of the current set (tools/summarize_profile.py),
+    or None."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", f"{PROFILE_TAG}_{cfg}_*.json"))):
+        d = json.load(open(f))
+        if kernel.split("::")[-1] in d.get("kernel", "") and d.get("valu_issue_util") is not None:
+            sq = d.get("sq", {})
+            return {"valu_issue_util": round(d["valu_issue_util"], 3),
+                    "lds_conflict_cycles_per_op": round(sq.get("SQ_LDS_BANK_CONFLICT", 0.0) /
+                                                        max(sq.get("SQ_INSTS_LDS", 1.0), 1.0), 3),
+                    "source": os.path.relpath(f, REPO)}
+    return None
+
+
 def profiled_traffic(cfg, kernel):
     """HBM bytes per launch from the newest rocprofv3 PMC summary in profiles/
     for this config and kernel (FETCH_SIZE x2 + WRITE_SIZE, KiB -> B;
@@ -537,7 +553,10 @@ def main():
                          "traffic_same_build": None if traffic_sha is None else traffic_sha == lib_sha16(),
                          "kernel": MODES[args.mode][1], "kernel_ms": round(kern_ms, 4),
                          "algorithmic_bytes_per_frame": BYTES_PER_FRAME,
-                         "algorithmic_bytes_per_launch": n_gran * BYTES_PER_GRANULE},
+                         "algorithmic_bytes_per_launch": n_gran * BYTES_PER_GRANULE,
+                         # what binds instead (DESIGN.md "Roofline"): VALU issue and
+                         # latency; the profiled SQ counters of the same kernel
+                         "issue": profiled_issue(args.config, MODES[args.mode][1])},
             "modes": {m: {"value": round(r["value"], 1), "kernel_ms": round(r["kernel_ms"], 4),
                           "kernel": MODES[m][1], "pcm": MODES[m][0]} for m, r in res.items()},
         }
