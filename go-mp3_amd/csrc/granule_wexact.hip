@@ -156,19 +156,31 @@ __device__ __forceinline__ void imdct_exact_s(const float x[18], int bt, const f
 
 // V = synthNWin * S of one time slot in the reference's order: the 32
 // distinct values X[m] to their ring columns and V[16] to column 32.
-__device__ __forceinline__ void matrix_exact_v16(float* colu) {
+// J (wave-uniform): every subband j >= J has S = +-0 in every slot of both
+// channels.  Its terms c * S[j] are +-0, and adding +-0 to a sum that started
+// from +0 leaves it unchanged bit for bit (such a sum is never -0, and
+// +0 + -0 = +0), so the 33 sums stop after the last block of four subbands
+// below J: the zero subbands above the coded bandwidth (count1, the encoder's
+// lowpass) cost nothing.  The sums advance together, four subbands at a time.
+__device__ __forceinline__ void matrix_exact_v16(float* colu, int J) {
 #pragma clang fp contract(off)
-  float S[32];
-#pragma unroll
-  for (int j = 0; j < 32; j++) S[j] = colu[kSlots * j];
   const float z0 = ozero();
+  float acc[33];
 #pragma unroll
-  for (int m = 0; m < 33; m++) {
-    float s = z0;
+  for (int m = 0; m < 33; m++) acc[m] = z0;
 #pragma unroll
-    for (int j = 0; j < 32; j++) s = s + kXNrow[m][j] * S[j];
-    colu[kSlots * (m < 32 ? dct32::kPosOfM[m] : kColV16)] = s;
+  for (int jb = 0; jb < 32; jb += 4) {
+    if (jb >= J) break;  // wave-uniform
+    float S[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) S[i] = colu[kSlots * (jb + i)];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+      for (int m = 0; m < 33; m++) acc[m] = acc[m] + kXNrow[m][jb + i] * S[i];
   }
+#pragma unroll
+  for (int m = 0; m < 33; m++) colu[kSlots * (m < 32 ? dct32::kPosOfM[m] : kColV16)] = acc[m];
 }
 
 // V[i] of the slot at x (the reference's value, bit for bit: 0 - x, not -x,
@@ -305,8 +317,18 @@ granule_wexact_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, c
 #pragma unroll
       for (int j = 0; j < 18; j++) s.ring[ch][k][kHist + j] = o[j];
     }
+    // J = 1 + the highest subband with a non-zero S in either channel
+    int J;
+    {
+      bool nz = false;
+#pragma unroll
+      for (int j = 0; j < 18; j++) nz |= o[j] != 0.0f;
+      const uint64_t b = __builtin_amdgcn_ballot_w64(act && nz);
+      const uint32_t m = (uint32_t)b | (uint32_t)(b >> 32);
+      J = m ? 32 - __builtin_clz(m) : 0;
+    }
     wave_sync();
-    if (need_v && act && (lane & 31) < 18) matrix_exact_v16(&s.ring[ch][0][kHist + (lane & 31)]);
+    if (need_v && act && (lane & 31) < 18) matrix_exact_v16(&s.ring[ch][0][kHist + (lane & 31)], J);
     wave_sync();
     if (more && lane < 10) {
       reinterpret_cast<uint4*>(&s.desc)[lane] = reinterpret_cast<const uint4*>(&s.descn)[lane];
