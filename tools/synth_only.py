@@ -24,7 +24,7 @@ gen = torch.Generator(device=dev)
 gen.manual_seed(7)
 d_l = torch.randn(n, 2, 576, device=dev, generator=gen) * 0.05
 d_p = torch.empty(n * 1152, dtype=torch.int16, device=dev)
-plan = mp3g.Plan(s, mode=mp3g.MODE_FAST)
+plan = mp3g.Plan(s, granules_per_chunk=int(os.environ.get("SYNTH_CHUNK", "0")), mode=mp3g.MODE_FAST)
 h = torch.cuda.current_stream().cuda_stream
 for _ in range(2):
     plan.synth_execute(d_g, d_l, d_p, stream=h)
