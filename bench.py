@@ -33,6 +33,12 @@ sys.path.insert(0, os.path.join(REPO, "go-mp3_amd"))
 BYTES_PER_GRANULE = 2 * 576 * 2 + 160 + 576 * 2 * 2
 BYTES_PER_FRAME = 2 * BYTES_PER_GRANULE  # MPEG-1 frame (2 granules)
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+# the DSP path is FP32-VALU-bound, report the flop roof beside
+# the HBM one: ~550 kflop per MPEG-1 stereo frame counted in the reference's
+# operation order (the fast kernel's transforms do fewer), against 157.3 TF/s
+# of FP32 with FMA; exact mode rounds every product and sum (no FMA): half that
+FLOPS_PER_FRAME = 550e3
+FP32_PEAK_TFLOPS = 157.3
 METRIC = "MP3 frames/sec (44.1 kHz stereo 128 kbps) at 1/2/4/8 GPUs; max |ΔPCM| LSB"
 
 
@@ -558,7 +564,14 @@ def main():
                          # latency; the profiled SQ counters of the same kernel
                          "issue": profiled_issue(args.config, MODES[args.mode][1])},
             "modes": {m: {"value": round(r["value"], 1), "kernel_ms": round(r["kernel_ms"], 4),
-                          "kernel": MODES[m][1], "pcm": MODES[m][0]} for m, r in res.items()},
+                          "kernel": MODES[m][1], "pcm": MODES[m][0],
+                          # SURVEY.md 8(d) flop roof (reference-order flops; exact: no-FMA ceiling)
+                          "flop_roofline": {
+                              "achieved_tflops": round(r["value"] / world * FLOPS_PER_FRAME / 1e12, 2),
+                              "peak_tflops": FP32_PEAK_TFLOPS if m == "fast" else FP32_PEAK_TFLOPS / 2,
+                              "frac": round(r["value"] / world * FLOPS_PER_FRAME / 1e12 /
+                                            (FP32_PEAK_TFLOPS if m == "fast" else FP32_PEAK_TFLOPS / 2), 4),
+                              "flops_per_frame": FLOPS_PER_FRAME}} for m, r in res.items()},
         }
         if out["roofline"]["traffic_same_build"] is False:
             print("bench.py: warning: roofline traffic is from a profile of another build (%s)" % traffic_src,
