@@ -571,7 +571,8 @@ def main():
                               "peak_tflops": FP32_PEAK_TFLOPS if m == "fast" else FP32_PEAK_TFLOPS / 2,
                               "frac": round(r["value"] / world * FLOPS_PER_FRAME / 1e12 /
                                             (FP32_PEAK_TFLOPS if m == "fast" else FP32_PEAK_TFLOPS / 2), 4),
-                              "flops_per_frame": FLOPS_PER_FRAME}} for m, r in res.items()},
+                              "flops_per_frame": FLOPS_PER_FRAME} if args.config != "c5" else None}
+                      for m, r in res.items()},  # (c5: MPEG-2 mono frames, another flop count)
         }
         if out["roofline"]["traffic_same_build"] is False:
             print("bench.py: warning: roofline traffic is from a profile of another build (%s)" % traffic_src,
