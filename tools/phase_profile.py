@@ -19,17 +19,9 @@ def device_workload(cfg):
     """bench.py's workload for cfg as device tensors (granules, coefficients, PCM out) + streams."""
     dev = torch.device("cuda:0")
     g, c, streams, info = bench.build_workload(cfg, 0)
-    if cfg == "c3":
-        pg, pc, idx = g
-        d_g = torch.from_numpy(pg.view(np.uint8).reshape(len(pg), -1).copy()).to(dev).index_select(
-            0, torch.from_numpy(idx).to(dev)).reshape(-1).contiguous()
-        d_c = torch.from_numpy(pc.reshape(len(pc), -1).copy()).to(dev).index_select(
-            0, torch.from_numpy(idx).to(dev)).reshape(-1).contiguous()
-        n = len(idx)
-    else:
-        d_g = torch.from_numpy(g.view(np.uint8).copy()).to(dev)
-        d_c = torch.from_numpy(c.reshape(-1).copy()).to(dev)
-        n = len(g)
+    d_g = torch.from_numpy(g.view(np.uint8).copy()).to(dev)
+    d_c = torch.from_numpy(c.reshape(-1).copy()).to(dev)
+    n = len(g)
     return d_g, d_c, torch.empty(n * 1152, dtype=torch.int16, device=dev), streams
 
 
