@@ -1447,9 +1447,14 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     //      before the PCM stores are issued -- vmcnt counts loads and stores in
     //      issue order, so a wait for the prefetch after the stores would wait
     //      for the stores too ----
-    if (more && lane < 10) {
-      reinterpret_cast<uint4*>(&s.desc)[lane] = reinterpret_cast<const uint4*>(&s.descn)[lane];
-      reinterpret_cast<uint4*>(&s.descn)[lane] = pd;
+    // (lane recomputed: the two LDS addresses kept live across the granule
+    // were spilled, and a scratch reload here waits for the PCM stores)
+    if (more) {
+      const int l = lane_fresh();
+      if (l < 10) {
+        reinterpret_cast<uint4*>(&s.desc)[l] = reinterpret_cast<const uint4*>(&s.descn)[l];
+        reinterpret_cast<uint4*>(&s.descn)[l] = pd;
+      }
     }
 
     // ---- 16-tap window over the X ring -> s16 PCM, stored straight to HBM ----

@@ -1,0 +1,19 @@
+# Round 3: band exponents filled one granule ahead (ping-pong expo buffers) and
+# the descriptor hand-over without spilled LDS addresses, vs the r03d build.
+set -u
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+L=$PWD/go-mp3_amd/mp3g
+A=${1:-libmp3g_base.so}; B=${2:-libmp3g_ex2.so}
+MP3G_LIB=$L/$B timeout -k 10 300 python -u -m pytest tests/test_gpu_fast.py -x -q --timeout 120 --timeout-method thread > gpurun_out/ex_pytest.log 2>&1 || { tail -30 gpurun_out/ex_pytest.log; exit 1; }
+tail -1 gpurun_out/ex_pytest.log
+for rep in 1 2 3; do
+  for lib in $A $B; do
+    MP3G_LIB=$L/$lib timeout -k 10 300 python bench.py --config c3 --steps 10 --warmup 3 --single-mode --no-cpu-baseline --no-bitstream --no-polyphase --no-c2 > gpurun_out/ex_${lib}.log 2>&1 || { tail -5 gpurun_out/ex_${lib}.log; exit 1; }
+    tail -1 gpurun_out/ex_${lib}.log | python -c "import json,sys;d=json.loads(sys.stdin.read());print('c3','"$lib"',d['value'],d['roofline']['kernel_ms'],d['modes']['fast'].get('max_dpcm_lsb'))"
+  done
+done
+for lib in $A $B; do
+  MP3G_LIB=$L/$lib timeout -k 10 300 python bench.py --config c2 --steps 20 --warmup 3 --single-mode --no-cpu-baseline --no-bitstream --no-polyphase > gpurun_out/exc2_${lib}.log 2>&1 || { tail -5 gpurun_out/exc2_${lib}.log; exit 1; }
+  tail -1 gpurun_out/exc2_${lib}.log | python -c "import json,sys;d=json.loads(sys.stdin.read());print('c2','"$lib"',d['value'],d['roofline']['kernel_ms'])"
+done
