@@ -65,6 +65,8 @@ void build_tables(DspTables* t);
 //   The window sum pcm[i] = sum_j D[32j+i] * (j even ? V_j[i] : V_j[32+i])
 //   reads X_j[a_i] (j even) and X_j[b_i] (j odd) with the signs folded into
 //   dwin[i][j] (a_i = 16+i | 48-i, b_i = 16-i | i-16).
+// slots per ring column of the fast kernel (granule_fast.hip kSlots)
+constexpr int kFastRingSlots = 34;
 struct FastTables {
   float c36[18][18];   // distinct cosN36 columns (= DspTables::cos36_distinct)
   float cos12[6][12];
@@ -88,6 +90,11 @@ struct FastTables {
   // (5..8), window of the reorder SOURCE line (9..10), the line's own
   // window in window-major order (11..12), reorder source line (13..22)
   uint32_t linfo[kCombos][576];
+  // the same for short, non-mixed blocks, pre-resolved for the fast kernel's
+  // reorder gather: short band (bits 0..3), 3 band + window of the source line
+  // (4..9) and of the line itself (10..15), the source line's int16 index in
+  // the staged ring (16..27: 2 kFastRingSlots (src / 18) + src % 18)
+  uint32_t sinfo[kCombos][576];
   // per (combo, subband): long band of the subband's first line (bits 0..4)
   // and a mask of the lines j = 1..17 that start a new long band (bits 5+j)
   uint32_t lband[kCombos][32];

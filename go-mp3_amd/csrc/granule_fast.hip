@@ -101,6 +101,7 @@ constexpr int kHist = 16;
 #define MP3G_FAST_WAVES_PER_SIMD 4
 #endif
 constexpr int kSlots = kHist + 18;
+static_assert(kSlots == kFastRingSlots, "FastTables::sinfo indexes the staged ring");
 #ifndef MP3G_FAST_DWIN_STRIDE
 #define MP3G_FAST_DWIN_STRIDE 20
 #endif
@@ -992,7 +993,9 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
   };
   __shared__ SharedSmem sh;
   __shared__ WaveSmem wsm[kWaves];
-  {
+  // the workgroup's tables, filled after each wave has issued its first
+  // loads: their latencies overlap
+  auto shared_init = [&]() {
     const int t = threadIdx.x;
     for (int e = t; e < 4 * 2 * 9; e += kLanes * kWaves) {
       const int bt = e / 18, par = (e / 9) & 1, q = e % 9;
@@ -1005,13 +1008,16 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     for (int e = t; e < 16; e += kLanes * kWaves) (&sh.isr[0][0])[e] = e < 14 ? (&g_fast.is_ratio[0][0])[e] : 1.0f;
     for (int e = t; e < 32 * 16; e += kLanes * kWaves) sh.dwin[e >> 4][e & 15] = (&g_fast.dwin[0][0])[e] * 32767.0f;
     for (int e = t; e < kCombos * 32; e += kLanes * kWaves) (&sh.lband[0][0])[e] = (&g_fast.lband[0][0])[e];
-  }
-  __syncthreads();  // the only workgroup barrier: the waves are independent from here on
+  };
   const int lane = threadIdx.x & (kLanes - 1);
   // wave-uniform in an SGPR: the chunk descriptor then comes in by scalar
   // loads and its fields (pointers, counts) stay out of the VGPR budget
   const uint32_t ci = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + (threadIdx.x >> 6));
-  if (ci >= n_chunks) return;
+  if (ci >= n_chunks) {  // (wave-uniform: one barrier per wave either way)
+    shared_init();
+    __syncthreads();
+    return;
+  }
   WaveSmem& s = wsm[threadIdx.x >> 6];
   const ChunkDesc cd = chunks[ci];
   const int ch = lane >> 5, k = lane & 31;
@@ -1029,6 +1035,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
   const uint32_t out_first = __builtin_amdgcn_readfirstlane((uint32_t)cd.out_first);
   const uint32_t end = __builtin_amdgcn_readfirstlane((uint32_t)(cd.out_first + cd.n_out));
   const mp3g_state* sin = state_in ? state_in + cd.stream : nullptr;
+
 
   // entry state: overlap store in registers, V history as X vectors
   // IMDCT overlap `store` (frame.go:473-476) in registers as pairs
@@ -1060,11 +1067,83 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     if (lane < 10 && w + 1 < end)
       reinterpret_cast<uint4*>(&s.descn)[lane] = reinterpret_cast<const uint4*>(gran + w + 1)[lane];
   }
-  wave_sync();
+  shared_init();
+  __syncthreads();  // the only workgroup barrier: the waves are independent from here on
 
   // PCM of a granule: one dword (L, R) per lane and slot pair
   uint32_t pk[9] = {};
   const int hi = lane >> 5;
+
+  // ---- 16-tap window over the X ring -> s16 PCM, stored straight to HBM ----
+  // (lanes of an absent channel compute values that are never stored; the
+  // PCM stores are issued for replayed granules too, through a resource with
+  // no records)
+  auto window_store = [&](uint32_t g, bool out, int nch) {
+    if (out) {
+      float dw[16];
+      {
+        const float4* d4 = reinterpret_cast<const float4*>(&sh.dwin[k][0]);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const float4 v = d4[q];
+          dw[4 * q] = v.x;
+          dw[4 * q + 1] = v.y;
+          dw[4 * q + 2] = v.z;
+          dw[4 * q + 3] = v.w;
+        }
+      }
+      // accumulator pair p = output slots (2p, 2p+1).  Tap 2t of the pair reads
+      // column a of rows (v, v+1) and tap 2t+1 column b of rows (v-1, v),
+      // v = 2p - 2t: every operand pair is two rows of one column, i.e. one
+      // ds_read2_b32 that lands as the packed operand, and each feeds up to 8
+      // accumulator pairs.
+      const f2* RA = reinterpret_cast<const f2*>(&s.ring[ch][pa][0]);
+      const float* RB = &s.ring[ch][pb][0];
+      f2 acc2[9];
+#pragma unroll
+      for (int p = 0; p < 9; p++) acc2[p] = bcast(0.0f);
+#pragma unroll
+      for (int v = -14; v <= 16; v += 2) {
+        const f2 A = RA[(kHist + v) / 2];  // slots (16+v, 17+v): 8-B aligned
+        const f2 B = {RB[kHist + v - 1], RB[kHist + v]};
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+          const int p = v / 2 + t;
+          if (p >= 0 && p < 9) {
+            acc2[p] = pfma(bcast(dw[2 * t]), A, acc2[p]);
+            acc2[p] = pfma(bcast(dw[2 * t + 1]), B, acc2[p]);
+          }
+        }
+      }
+      // (L, R) sample pairs without LDS staging: one v_permlane32_swap per slot
+      // pair hands lane i slot 2p's (L, R) and lane 32 + i slot 2p + 1's, so
+      // every lane stores one dword per slot pair and the wave 2 x 128
+      // contiguous bytes.  Mono: the swap hands lane i channel 0's slot 2p and
+      // lane 32 + i its slot 2p + 1, stored in both halves (frame.go:671-678).
+      auto pack = [&](auto mono) {
+#pragma unroll
+        for (int p = 0; p < 9; p++) {
+          const int a = (int)__builtin_amdgcn_fmed3f(acc2[p].x, -32767.0f, 32767.0f);
+          const int b = (int)__builtin_amdgcn_fmed3f(acc2[p].y, -32767.0f, 32767.0f);
+          const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+          // low halves of (r[0], r[1]) -> one dword: L | R << 16 (R = L for mono)
+          pk[p] = __builtin_amdgcn_perm((uint32_t)(decltype(mono)::value ? r[0] : r[1]), (uint32_t)r[0], 0x05040100u);
+        }
+      };
+      if (nch == 2) pack(std::false_type{});
+      else pack(std::true_type{});
+      // stored right away: a store's data registers are free again once it
+      // has issued (no s_waitcnt before their reuse on gfx950), and the loads
+      // this wave waits for next were issued before these stores
+    }
+    {
+      const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
+          pcm + (size_t)g * 1152, (short)0, out && !MP3G_TIMING_NOSTORE ? MP3G_PCM_BYTES_PER_GRANULE : 0, 0x00020000);
+#pragma unroll
+      for (int p = 0; p < 9; p++)
+        __builtin_amdgcn_raw_buffer_store_b32(pk[p], rp, 4 * (32 * (2 * p + hi) + k), 0, 2);  // non-temporal: c2 -1.9 %, c3 -0.8 %
+    }
+  };
 
   if constexpr (kStamp) {
     tprev = __builtin_amdgcn_s_memtime();
@@ -1155,7 +1234,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       // lines 1..j.  Every long band starts at an even line (consts.go:68-97
       // SfBandIndices; dsp_tables.cpp checks it), so lines 2q and 2q + 1
       // share one band: one exponent read per line pair.
-      const uint32_t lb = sh.lband[combo][k];
+      const uint32_t lb = sh.lband[combo][lane_fresh() & 31];  // (lane recomputed: no spilled address)
       _Float16 ex[9];
 #pragma unroll
       for (int q = 0; q < 9; q++)
@@ -1181,26 +1260,53 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       const int16_t* rch = reinterpret_cast<const int16_t*>(&s.ring[ch][0][kHist]);
       // line info through a buffer resource (SGPR base, 32-bit lane offset) and
       // the lane's first line recomputed here: nothing of this rare path stays
-      // live (in VGPRs) across the granule loop
+      // live (in VGPRs) across the granule loop.  Short, non-mixed blocks in
+      // every channel (wave-uniform) take the pre-resolved table sinfo.
+      auto plain = [&](uint32_t d) { return is_short(d) && !(d >> 24); };
+      const bool plain_short = plain(cp1[0]) && (nch == 1 || plain(cp1[1]));
       const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
-          const_cast<uint32_t*>(&g_fast.linfo[combo][0]), (short)0, 576 * 4, 0x00020000);
+          const_cast<uint32_t*>(plain_short ? &g_fast.sinfo[combo][0] : &g_fast.linfo[combo][0]), (short)0,
+          576 * 4, 0x00020000);
       const int L0 = 18 * (lane_fresh() & 31);
+      // all 18 words first, as 9 8-B loads: one wait, not one per line
+      uint32_t infw[18];
 #pragma unroll
-      for (int j = 0; j < 18; j++) {
-        const int L = L0 + j;
-        const uint32_t inf = __builtin_amdgcn_raw_buffer_load_b32(rl, 4 * L, 0, 0);
-        const int sfl = inf & 31, sfs = (inf >> 5) & 15, wsrc = (inf >> 9) & 3, wown = (inf >> 11) & 3;
-        const int srcr = inf >> 13;
-        const bool longlike = !shortblk || (mixed && L < 36);
-        const bool started = sfs < nsfs;
-        const bool reord = sfs == (mixed ? 3 : 0) || started;
-        const int src = seli(longlike || !reord, L, srcr);
-        const int win = seli(reord, wsrc, wown);
-        const int eidx = seli(longlike, 22 * ch + sfl, 44 + 39 * ch + 3 * sfs + win);
-        const bool process = longlike ? (shortblk || L < count1) : started;
-        const int sk = (src * 3641) >> 16;  // src / 18 for src < 576
-        const int xi = rch[2 * kSlots * sk + (src - 18 * sk)];
-        x[j] = self(process, requant_fast(xi, s.expo[eidx]), (float)xi);
+      for (int q = 0; q < 9; q++) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(rl, 4 * L0 + 8 * q, 0, 0);
+        infw[2 * q] = v[0];
+        infw[2 * q + 1] = v[1];
+      }
+      if (plain_short) {
+        // (the general loop of the else branch with longlike = false, mixed = false)
+        const int ebase = 44 + 39 * ch;
+#pragma unroll
+        for (int j = 0; j < 18; j++) {
+          const uint32_t inf = infw[j];
+          const int sfs = inf & 15u;
+          const bool started = sfs < nsfs;
+          const bool reord = sfs == 0 || started;
+          const int xi = rch[seli(reord, (int)(inf >> 16), 2 * kSlots * (lane_fresh() & 31) + j)];
+          const int e = seli(reord, (int)((inf >> 4) & 63u), (int)((inf >> 10) & 63u));
+          x[j] = self(started, requant_fast(xi, s.expo[ebase + e]), (float)xi);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 18; j++) {
+          const int L = L0 + j;
+          const uint32_t inf = infw[j];
+          const int sfl = inf & 31, sfs = (inf >> 5) & 15, wsrc = (inf >> 9) & 3, wown = (inf >> 11) & 3;
+          const int srcr = inf >> 13;
+          const bool longlike = !shortblk || (mixed && L < 36);
+          const bool started = sfs < nsfs;
+          const bool reord = sfs == (mixed ? 3 : 0) || started;
+          const int src = seli(longlike || !reord, L, srcr);
+          const int win = seli(reord, wsrc, wown);
+          const int eidx = seli(longlike, 22 * ch + sfl, 44 + 39 * ch + 3 * sfs + win);
+          const bool process = longlike ? (shortblk || L < count1) : started;
+          const int sk = (src * 3641) >> 16;  // src / 18 for src < 576
+          const int xi = rch[2 * kSlots * sk + (src - 18 * sk)];
+          x[j] = self(process, requant_fast(xi, s.expo[eidx]), (float)xi);
+        }
       }
       wave_sync();  // staged lines read before the slots are reused
     }
@@ -1270,9 +1376,16 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
         } else {
           const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
               const_cast<uint32_t*>(&g_fast.linfo[combo][0]), (short)0, 576 * 4, 0x00020000);
+          uint32_t infw[18];  // (9 8-B loads, one wait)
+#pragma unroll
+          for (int q = 0; q < 9; q++) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b64(rl, 4 * 18 * k0 + 8 * q, 0, 0);
+            infw[2 * q] = v[0];
+            infw[2 * q + 1] = v[1];
+          }
 #pragma unroll
           for (int j = 0; j < 18; j++) {
-            const uint32_t info = __builtin_amdgcn_raw_buffer_load_b32(rl, 4 * (18 * k0 + j), 0, 0);
+            const uint32_t info = infw[j];
             const int sfl = info & 31, sfs = (info >> 5) & 15, wown = (info >> 11) & 3;
             const bool lp = mixed0 && sfl < 8 && sfl >= nl_is;
             const bool sp = sfs < 12 && (!mixed0 || sfs >= 3) && sfs >= ns_is;
@@ -1457,73 +1570,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       }
     }
 
-    // ---- 16-tap window over the X ring -> s16 PCM, stored straight to HBM ----
-    // (lanes of an absent channel compute values that are never stored)
-    if (out) {
-      float dw[16];
-      {
-        const float4* d4 = reinterpret_cast<const float4*>(&sh.dwin[k][0]);
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-          const float4 v = d4[q];
-          dw[4 * q] = v.x;
-          dw[4 * q + 1] = v.y;
-          dw[4 * q + 2] = v.z;
-          dw[4 * q + 3] = v.w;
-        }
-      }
-      // accumulator pair p = output slots (2p, 2p+1).  Tap 2t of the pair reads
-      // column a of rows (v, v+1) and tap 2t+1 column b of rows (v-1, v),
-      // v = 2p - 2t: every operand pair is two rows of one column, i.e. one
-      // ds_read2_b32 that lands as the packed operand, and each feeds up to 8
-      // accumulator pairs.
-      const f2* RA = reinterpret_cast<const f2*>(&s.ring[ch][pa][0]);
-      const float* RB = &s.ring[ch][pb][0];
-      f2 acc2[9];
-#pragma unroll
-      for (int p = 0; p < 9; p++) acc2[p] = bcast(0.0f);
-#pragma unroll
-      for (int v = -14; v <= 16; v += 2) {
-        const f2 A = RA[(kHist + v) / 2];  // slots (16+v, 17+v): 8-B aligned
-        const f2 B = {RB[kHist + v - 1], RB[kHist + v]};
-#pragma unroll
-        for (int t = 0; t < 8; t++) {
-          const int p = v / 2 + t;
-          if (p >= 0 && p < 9) {
-            acc2[p] = pfma(bcast(dw[2 * t]), A, acc2[p]);
-            acc2[p] = pfma(bcast(dw[2 * t + 1]), B, acc2[p]);
-          }
-        }
-      }
-      // (L, R) sample pairs without LDS staging: one v_permlane32_swap per slot
-      // pair hands lane i slot 2p's (L, R) and lane 32 + i slot 2p + 1's, so
-      // every lane stores one dword per slot pair and the wave 2 x 128
-      // contiguous bytes.  Mono: the swap hands lane i channel 0's slot 2p and
-      // lane 32 + i its slot 2p + 1, stored in both halves (frame.go:671-678).
-      auto pack = [&](auto mono) {
-#pragma unroll
-        for (int p = 0; p < 9; p++) {
-          const int a = (int)__builtin_amdgcn_fmed3f(acc2[p].x, -32767.0f, 32767.0f);
-          const int b = (int)__builtin_amdgcn_fmed3f(acc2[p].y, -32767.0f, 32767.0f);
-          const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
-          // low halves of (r[0], r[1]) -> one dword: L | R << 16 (R = L for mono)
-          pk[p] = __builtin_amdgcn_perm((uint32_t)(decltype(mono)::value ? r[0] : r[1]), (uint32_t)r[0], 0x05040100u);
-        }
-      };
-      if (nch == 2) pack(std::false_type{});
-      else pack(std::true_type{});
-      // stored right away: a store's data registers are free again once it
-      // has issued (no s_waitcnt before their reuse on gfx950), and the loads
-      // this wave waits for next were issued before these stores
-    }
-    {
-      // issued for replayed granules too, through a resource with no records
-      const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
-          pcm + (size_t)g * 1152, (short)0, out && !MP3G_TIMING_NOSTORE ? MP3G_PCM_BYTES_PER_GRANULE : 0, 0x00020000);
-#pragma unroll
-      for (int p = 0; p < 9; p++)
-        __builtin_amdgcn_raw_buffer_store_b32(pk[p], rp, 4 * (32 * (2 * p + hi) + k), 0, 2);  // non-temporal: c2 -1.9 %, c3 -0.8 %
-    }
+    window_store(g, out, nch);
     wave_sync();  // ring reads done
     stamp(6);
 

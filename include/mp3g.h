@@ -358,9 +358,8 @@ int mp3g_decoder_skip_ns(mp3g_decoder* dec, int64_t delta_ns);
  * Runs a FAST-mode plan once through the s_memtime-instrumented build of the
  * fast kernel and returns, per kernel phase, the shader cycles summed over
  * all chunks (out_cycles[0..7]: parameters, requantize, stereo+antialias,
- * IMDCT, even/odd fold + matrixing of slots 0..8, of slots 9..17,
- * window+store, history shift).  PCM is
- * written as by mp3g_plan_execute.  Synchronous. */
+ * IMDCT, S rows into the ring, matrixing (DCT-32), window+store, history
+ * shift).  PCM is written as by mp3g_plan_execute.  Synchronous. */
 int mp3g_plan_debug_phases(mp3g_plan* plan, const mp3g_granule* d_granules, const int16_t* d_coeffs,
                            int16_t* d_pcm, uint64_t* out_cycles, void* hip_stream);
 /* The same instrumented launch; per chunk (out_ticks[4 * chunk + 0..3]) the

@@ -16,9 +16,17 @@ import mp3g  # noqa: E402
 
 
 def device_workload(cfg):
-    """bench.py's workload for cfg as device tensors (granules, coefficients, PCM out) + streams."""
+    """bench.py's workload for cfg as device tensors (granules, coefficients, PCM out) + streams.
+    cfg "c2:short" / "c2:long": every granule turned into short (block_type 2) /
+    long (block_type 0) blocks, to price the two block paths."""
     dev = torch.device("cuda:0")
+    cfg, _, force = cfg.partition(":")
     g, c, streams, info = bench.build_workload(cfg, 0)
+    if force:
+        ch = g["ch"]
+        ch["win_switch_flag"] = 1 if force == "short" else 0
+        ch["block_type"] = 2 if force == "short" else 0
+        ch["mixed_block_flag"] = 0
     d_g = torch.from_numpy(g.view(np.uint8).copy()).to(dev)
     d_c = torch.from_numpy(c.reshape(-1).copy()).to(dev)
     n = len(g)

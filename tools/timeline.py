@@ -31,7 +31,7 @@ e1.record(s)
 torch.cuda.synchronize()
 kern_us = e0.elapsed_time(e1) / 20 * 1e3
 t = plan.debug_timeline(d_g, d_c, d_pcm).astype(np.int64)
-np.save(os.path.join(REPO, "gpurun_out", f"timeline_{cfg}_{karg}.npy"), t)
+np.save(os.path.join(REPO, "gpurun_out", f"timeline_{cfg}_{karg}{os.environ.get('TL_TAG', '')}.npy"), t)
 t = (t - t[:, 0].min()) / 100.0  # 100 MHz ticks -> us
 q = lambda a: [round(float(np.percentile(a, p)), 2) for p in (0, 50, 90, 100)]
 print(json.dumps({"config": cfg, "chunks": len(t), "info": plan.info(), "kernel_us_events": round(kern_us, 2),
