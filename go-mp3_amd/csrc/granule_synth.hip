@@ -201,10 +201,24 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
   const mp3g_state* sin = state_in ? state_in + cd.stream : nullptr;
   synth_init_ring(s, sin, init_in, lane);
 
+  // channel counts of the chunk's granules as a stereo bit mask in SGPRs, 64
+  // granules per refill (one vector load and a ballot): the per-granule
+  // header reads were scalar loads whose wait held up the next granule's
+  // line loads
+  uint64_t smask = 0;
+  uint32_t mbase = 0xffffffffu;  // (no granule yet: the first call fills the mask)
+  auto nch_of = [&](uint32_t g) -> int {
+    if (g < mbase || g - mbase >= 64u) {
+      const uint32_t gi = g + (uint32_t)lane_fresh();
+      smask = __builtin_amdgcn_ballot_w64(gi < end && hdr_nch(gran[gi].header) == 2);
+      mbase = g;
+    }
+    return ((smask >> (g - mbase)) & 1u) ? 2 : 1;
+  };
   auto load = [&](uint32_t g, f2 v[9]) {
     const bool in = g < end;
     const uint32_t gg = in ? g : w;
-    const uint32_t nch = in ? hdr_nch(__builtin_amdgcn_readfirstlane(gran[gg].header)) : 0u;
+    const uint32_t nch = in ? (uint32_t)nch_of(gg) : 0u;
     synth_load(lines, gg, nch * 2304u, lane, v);
   };
   const int hi = lane >> 5;
@@ -243,7 +257,7 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
     else if (left4 > span2) __builtin_amdgcn_s_setprio(2);
     else if (left4 > span) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
-    const int nch = hdr_nch(__builtin_amdgcn_readfirstlane(gran[g].header));
+    const int nch = nch_of(g);
     const bool out = g >= out_first;
     // a hot granule: its zone is redone in the reference's order after the pass
 #if MP3G_HOT_CHECK
