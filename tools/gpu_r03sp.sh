@@ -1,0 +1,14 @@
+# Round 3: the first granule's lines loaded before the replay start is known
+# (speculative, reloaded on a mono/stereo walk-back) vs the previous commit.
+set -u
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+L=$PWD/go-mp3_amd/mp3g
+MP3G_LIB=$L/libmp3g_sp.so timeout -k 10 400 python -u -m pytest tests/test_gpu_fast.py tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread > gpurun_out/sp_pytest.log 2>&1 || { tail -30 gpurun_out/sp_pytest.log; exit 1; }
+tail -1 gpurun_out/sp_pytest.log
+for rep in 1 2 3; do
+  for lib in libmp3g_head.so libmp3g_sp.so; do
+    MP3G_LIB=$L/$lib timeout -k 10 300 python bench.py --config c2 --steps 20 --warmup 3 --single-mode --no-cpu-baseline --no-bitstream --no-polyphase > gpurun_out/sp_${lib}.log 2>&1 || { tail -5 gpurun_out/sp_${lib}.log; exit 1; }
+    tail -1 gpurun_out/sp_${lib}.log | python -c "import json,sys;d=json.loads(sys.stdin.read());print('c2','"$lib"',d['value'],d['roofline']['kernel_ms'])"
+  done
+done
