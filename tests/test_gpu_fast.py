@@ -103,6 +103,24 @@ def test_fast_state_continuation(gpu):
     assert_close(p4, want[cut:], "exact state -> fast")
 
 
+@pytest.mark.parametrize("mode", [synth.MODE_JOINT, synth.MODE_MONO])
+def test_all_short_blocks(gpu, mode):
+    """Every granule a short, non-mixed block (the fast kernel's pre-resolved
+    reorder table, FastTables::sinfo): fast within +-1 LSB and exact mode
+    bit-identical, with MS / IS in the joint-stereo case."""
+    g, c, s = synth.synth_batch(4, 40, seed=21, mode=mode, p_is=0.5)
+    ch = g["ch"]
+    ch["win_switch_flag"] = 1
+    ch["block_type"] = 2
+    ch["mixed_block_flag"] = 0
+    assert gpu.validate(g, c)[0] == 0
+    want, _ = oracle.dsp_streams(g, c, s)
+    pcm, _ = fast_plan(gpu, g, c, s, chunk=5)
+    assert_close(pcm, want, "all short, fast")
+    pcm, _ = run_plan(gpu, g, c, s, chunk=5)
+    assert np.array_equal(pcm, want), "all short, exact"
+
+
 def test_fast_edge_cases(gpu):
     g, c, s = synth.synth_batch(3, 10, seed=5)
     g0, c0 = g.copy(), np.zeros_like(c)
