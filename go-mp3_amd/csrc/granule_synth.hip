@@ -67,10 +67,17 @@ struct __align__(16) SynthWaveSmem {
 
 namespace {
 
-// The granule's lines as 8-B pairs: pair p = lane + 64 r of [nch][576].
+// The granule's lines [nch][576] (1,152 floats): lane's quads lane + 64 r
+// (r < 4, floats 0..1023) as 16-B loads and the pair 512 + lane (floats
+// 1024..1151) as an 8-B load, held as nine pairs: buf[2 r], buf[2 r + 1] the
+// halves of quad r, buf[8] the tail pair.  (Nine 8-B loads before.)
 // Issued unconditionally (straight-line vmcnt accounting): past the chunk
 // (or with nbytes 0) the resource has no records, so the loads return 0 and
 // touch no memory.
+// first line in [2][576] of pair i (0..8) of this lane
+__device__ __forceinline__ int synth_pair_line(int lane, int i) {
+  return i < 8 ? 4 * (lane + 64 * (i >> 1)) + 2 * (i & 1) : 1024 + 2 * lane;
+}
 __device__ __forceinline__ void synth_load(const float* lines, uint32_t g, uint32_t nbytes, int lane, f2 v[9]) {
   const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(lines + (size_t)g * MP3G_COEF_PER_GRANULE), (short)0, MP3G_TIMING_NOLOAD ? 0 : (int)nbytes,
@@ -79,20 +86,22 @@ __device__ __forceinline__ void synth_load(const float* lines, uint32_t g, uint3
   // (the fused kernel's coefficient loads measured +0.9 % with it,
   // tools/gpu_r03nt.sh)
 #pragma unroll
-  for (int r = 0; r < 9; r++) {
-    const auto u = __builtin_amdgcn_raw_buffer_load_b64(rc, 8 * lane + 512 * r, 0, 2);
-    v[r] = (f2){__uint_as_float(u[0]), __uint_as_float(u[1])};
+  for (int r = 0; r < 4; r++) {
+    const auto u = __builtin_amdgcn_raw_buffer_load_b128(rc, 16 * lane + 1024 * r, 0, 2);
+    v[2 * r] = (f2){__uint_as_float(u[0]), __uint_as_float(u[1])};
+    v[2 * r + 1] = (f2){__uint_as_float(u[2]), __uint_as_float(u[3])};
   }
+  const auto u = __builtin_amdgcn_raw_buffer_load_b64(rc, 4096 + 8 * lane, 0, 2);
+  v[8] = (f2){__uint_as_float(u[0]), __uint_as_float(u[1])};
 }
 
 // stage: line 18 sb + ss of channel c -> ring[c][sb][cur + ss] (cur: the
-// first slot of the current half), as 8-B pairs (ds_write_b64, 4 x 16 lanes:
-// as separate dwords the 32 lanes of a write group land on 16 even banks)
+// first slot of the current half), as 8-B pairs (ds_write_b64)
 template <int cur>
 __device__ __forceinline__ void synth_stage(SynthWaveSmem& s, const f2 buf[9], int nch) {
 #pragma unroll
   for (int r = 0; r < 9; r++) {
-    const int e = 2 * lane_fresh() + 128 * r;  // first line of the pair in [2][576]
+    const int e = synth_pair_line(lane_fresh(), r);  // first line of the pair in [2][576]
     const int c = e >= 576;
     const int l = e - 576 * c;
     const int sb = (l * 3641) >> 16;  // l / 18 for l < 576
