@@ -341,7 +341,7 @@ def polyphase_leg(args, rank, dev, stream, d_g, streams, n_gran, local):
     return out
 
 
-PROFILE_TAG = "r03f"  # profiles/<tag>_<cfg>_<kernel>.json of the current kernels
+PROFILE_TAG = "r03g"  # profiles/<tag>_<cfg>_<kernel>.json of the current kernels
 
 
 def profiled_issue(cfg, kernel):
