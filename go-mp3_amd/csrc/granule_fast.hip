@@ -54,6 +54,9 @@ namespace v3 {
 // tables.  8 waves: 2 workgroups (16 waves) per CU, the shared tables held
 // twice per CU instead of four times (2-3 % faster than 4-wave workgroups on
 // c2 and c3, tools/gpu_ab.sh; 16 waves measured the same).
+#ifndef MP3G_FAST_PRIO
+#define MP3G_FAST_PRIO 1  // progress-balanced s_setprio (0: A/B experiments)
+#endif
 #ifndef MP3G_FAST_WG_WAVES
 #define MP3G_FAST_WG_WAVES 8
 #endif
@@ -1158,7 +1161,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
   const uint32_t span = end - w, span2 = 2 * span, span3 = 3 * span;
   uint32_t nz = 0;  // hot zones recorded (s.zone)
   for (uint32_t g = w; g < end; g++) {
-    {
+    if (MP3G_FAST_PRIO) {
       const uint32_t left4 = 4u * (end - g);  // priority floor(4 * left / span), 3 .. 0
       if (left4 > span3) __builtin_amdgcn_s_setprio(3);
       else if (left4 > span2) __builtin_amdgcn_s_setprio(2);
