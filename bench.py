@@ -11,11 +11,17 @@ workload (default, --config c3 = BASELINE configs[2], the largest single-GPU
          stream (1 x 10,000 frames, granule-parallel) is timed beside it.
          --config c2 / c5: those configs as the headline.
 scaling: weak -- every rank decodes its own stream(s); no data-path collective
-         (value = frames of all ranks / max-over-ranks time).  --gather adds a
-         separately reported RCCL gather of the PCM to rank 0.
+         (value = frames of all ranks / max-over-ranks time).  With N > 1 the
+         PCM of every rank is then gathered to rank 0 (SURVEY.md 8(d) c4 /
+         8(e): point-to-point RCCL transfers over xGMI into one preallocated
+         buffer), timed and reported separately under "gather" (value stays
+         the kernel-only number); --no-gather skips it.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
-torch.distributed.run (one process per GPU, RCCL backend).
+torch.distributed.run (one process per GPU; --backend nccl = RCCL, the
+default, or gloo with the collectives staged through host memory -- the
+one-GPU rehearsal of the multi-rank path, tests/test_gpu_bench_dist.py).
+Ranks map to GPUs as LOCAL_RANK modulo the visible device count.
 """
 import argparse
 import json
@@ -61,7 +67,10 @@ def parse():
     ap.add_argument("--single-mode", action="store_true", help="time only --mode")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-repeats", type=int, default=5)
-    ap.add_argument("--gather", action="store_true", help="also time an RCCL PCM gather to rank 0")
+    ap.add_argument("--no-gather", action="store_true",
+                    help="N > 1: skip the timed PCM gather to rank 0 (reported separately, never in value)")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="N > 1: process-group backend (nccl = RCCL over xGMI; gloo stages through host memory)")
     ap.add_argument("--no-bitstream", action="store_true",
                     help="skip the bitstream leg (host scan + GPU Huffman + DSP on real Layer III streams)")
     ap.add_argument("--no-pipelined", action="store_true",
@@ -434,6 +443,71 @@ def time_plan(mp3g, streams, d_g, d_c, d_pcm, mode, chunk, local, steps, warmup,
     return wall, ev0.elapsed_time(ev1) / steps, pinfo
 
 
+def gather_leg(args, rank, world, dev, d_pcm, n_gran, mdist):
+    """the PCM of every rank to rank 0, timed apart
+    from the decode.  RCCL: point-to-point sends over xGMI straight into one
+    preallocated device buffer on rank 0 (mp3g.dist.gather_pcm).  gloo (the
+    one-GPU rehearsal): each rank's PCM staged to host memory first, gathered
+    into one preallocated host buffer.  A small gather first sets up the
+    peer connections (untimed).  Barrier + synchronize on both sides, max over
+    ranks.  Rank 0 then checks the first stream of every rank's slice against
+    the oracle on that rank's regenerated input (checker only)."""
+    import torch
+    import torch.distributed as dist
+    from mp3g import synth
+    gloo = args.backend == "gloo"
+    coll_dev = torch.device("cpu") if gloo else dev
+    nbytes = n_gran * 2304
+    sizes = [torch.zeros(1, dtype=torch.int64, device=coll_dev) for _ in range(world)]
+    dist.all_gather(sizes, torch.tensor([nbytes], dtype=torch.int64, device=coll_dev))
+    total = int(sum(int(x.item()) for x in sizes))
+    out = None
+    if rank == 0:
+        out = torch.empty(total // 2, dtype=torch.int16, device=coll_dev)
+        if gloo:
+            out = out.pin_memory()
+    warm = torch.zeros(1 << 16, dtype=torch.int16, device=coll_dev)
+    mdist.gather_pcm(warm, dst=0)
+    host = torch.empty(n_gran * 1152, dtype=torch.int16).pin_memory() if gloo else None
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    src = d_pcm
+    if gloo:
+        host.copy_(d_pcm)
+        src = host
+    mdist.gather_pcm(src, dst=0, out=out)
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    t_max = mdist.max_over_ranks(wall, device=coll_dev)
+    res = {"ms": round(1000.0 * t_max, 3), "bytes": total,
+           "GBps": round(total / t_max / 1e9, 2),
+           "into": "one preallocated %s buffer on rank 0 (mp3g.dist.gather_pcm)" % ("pinned host" if gloo else "device"),
+           "backend": "gloo (PCM staged through host memory)" if gloo else "RCCL point-to-point over xGMI",
+           "note": "not in value: value is the decode alone (SURVEY.md 8(d) c4)"}
+    if rank == 0 and not args.no_cpu_baseline and args.config in ("c2", "c3"):
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle  # checker of the gathered PCM only
+        pcm = out.cpu().numpy() if not gloo else out.numpy()
+        diffs, off = [], 0
+        per_rank = [int(x.item()) // 2304 for x in sizes]
+        for r in range(world):
+            if args.config == "c2":
+                g1, c1, s1 = synth.synth_batch(1, 10000, seed=1 + 1000003 * r)
+            else:  # the rank's first stream (seed 1 + 1024 r)
+                _, g1, c1, s1 = synth.encode_batch([1 + 1024 * r], 1024, n_threads=1)
+            want, _ = oracle.dsp_streams(g1, c1, s1)
+            got = pcm[off * 1152:(off + len(g1)) * 1152].reshape(-1, 576, 2)
+            diffs.append(dpcm(got, want))
+            off += per_rank[r]
+        res["parity"] = {"max_dpcm_lsb": max(diffs), "per_rank": diffs,
+                         "sample": "the first stream of every rank's slice of the gathered PCM vs the oracle"}
+    return res
+
+
 def dpcm(a, b):
     return int(np.abs(a.astype(np.int32) - b.astype(np.int32)).max(initial=0))
 
@@ -445,11 +519,18 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # (device_count does not initialise the GPU on this image)
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group("gloo")
     torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
+    # collectives of the timing rule run where the backend can: the GPU under
+    # RCCL, host memory under gloo
+    coll_dev = dev if args.backend == "nccl" else torch.device("cpu")
     import mp3g
     from mp3g import dist as mdist
 
@@ -471,7 +552,7 @@ def main():
         mode = mp3g.MODE_FAST if mode_name == "fast" else mp3g.MODE_EXACT
         wall, kern_ms, pinfo = time_plan(mp3g, streams, d_g, d_c, d_pcm, mode, args.chunk, local, args.steps,
                                          args.warmup, stream, world, dev)
-        t_max = mdist.max_over_ranks(wall, device=dev)
+        t_max = mdist.max_over_ranks(wall, device=coll_dev)
         frames_all = n_frames * world
         return {"value": frames_all * args.steps / t_max, "ms_per_step": 1000.0 * t_max / args.steps,
                 "kernel_ms": kern_ms, "chunks": pinfo["chunks"], "halo_granules": pinfo["halo_granules"],
@@ -504,7 +585,7 @@ def main():
         wall, kern_ms, pinfo = time_plan(mp3g, s2, d_g2, d_c2, d_p2, mp3g.MODE_FAST, 0, local, max(args.steps, 20),
                                          args.warmup, stream, world, dev)
         steps2 = max(args.steps, 20)
-        t_max = mdist.max_over_ranks(wall, device=dev)
+        t_max = mdist.max_over_ranks(wall, device=coll_dev)
         c2 = {"workload": "c2: 1 stream x 10,000 frames, 44.1 kHz stereo 128 kbps CBR (synthetic boundary input), "
                           "granule-parallel", "mode": MODES["fast"][0],
               "value": round(len(g2) // 2 * world * steps2 / t_max, 1), "ms_per_step": round(1000 * t_max / steps2, 4),
@@ -520,14 +601,9 @@ def main():
             c2["max_dpcm_lsb"] = dpcm(d_p2.cpu().numpy().reshape(-1, 576, 2), ref2)
         del d_g2, d_c2, d_p2
 
-    gather_ms = None
-    if args.gather and world > 1:
-        torch.cuda.synchronize(dev)
-        dist.barrier()
-        tg = time.perf_counter()
-        mdist.gather_pcm(d_pcm, dst=0)
-        torch.cuda.synchronize(dev)
-        gather_ms = 1000.0 * (time.perf_counter() - tg)
+    gather = None
+    if world > 1 and not args.no_gather:
+        gather = gather_leg(args, rank, world, dev, d_pcm, n_gran, mdist)
 
     if rank == 0:
         kern_ms = main_res["kernel_ms"]
@@ -577,14 +653,28 @@ def main():
         if out["roofline"]["traffic_same_build"] is False:
             print("bench.py: warning: roofline traffic is from a profile of another build (%s)" % traffic_src,
                   file=sys.stderr)
-        if gather_ms is not None:
-            out["gather_ms"] = round(gather_ms, 3)
+        if gather is not None:
+            out["gather_ms"] = gather["ms"]
+            out["gather"] = gather
         if bitstream is not None:
             out["bitstream"] = bitstream
         if polyphase is not None:
             out["polyphase"] = polyphase
         if c2 is not None:
             out["c2"] = c2
+        if world > 1 and not args.no_cpu_baseline and args.config in ("c2", "c3"):
+            # N > 1: parity of rank 0's timed output on its first
+            # --parity-streams streams (the CPU baseline is an N = 1 figure)
+            sys.path.insert(0, os.path.join(REPO, "oracle"))
+            import oracle  # checker of the timed output only
+            per = 2 * cfg_info["frames_per_stream"]
+            k = min(args.parity_streams, len(streams))
+            n_chk = per * k
+            ref = oracle.dsp_streams_mt(g[:n_chk], c[:n_chk], mp3g.streams_for([per] * k), CPU_THREADS)
+            for m, r in res.items():
+                out["modes"][m]["max_dpcm_lsb"] = dpcm(r["pcm"][:n_chk], ref)
+                out["modes"][m]["parity_granules"] = int(n_chk)
+            out["max_dpcm_lsb"] = out["modes"][args.mode]["max_dpcm_lsb"]
         if world == 1 and not args.no_cpu_baseline and args.config in ("c2", "c3"):
             sys.path.insert(0, os.path.join(REPO, "oracle"))
             import oracle  # CPU baseline leg + parity check of the timed output

@@ -35,14 +35,6 @@
 #include "dct4_18.h"
 #include "xlane.h"
 
-// timing-only builds (wrong PCM): drop the PCM stores / the coefficient or
-// line loads
-#ifndef MP3G_TIMING_NOSTORE
-#define MP3G_TIMING_NOSTORE 0
-#endif
-#ifndef MP3G_TIMING_NOLOAD
-#define MP3G_TIMING_NOLOAD 0
-#endif
 // cache policy of the PCM stores (2 = nt: streamed past the caches)
 #ifndef MP3G_PCM_STORE_AUX
 #define MP3G_PCM_STORE_AUX 2
@@ -159,7 +151,7 @@ constexpr uint32_t kZones = 8;
 __device__ __forceinline__ void load_lines(const int16_t* coef, uint32_t g, int lane, uint32_t cw[9],
                                            int nbytes = (int)(MP3G_COEF_PER_GRANULE * sizeof(int16_t))) {
   const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<int16_t*>(coef + (size_t)g * MP3G_COEF_PER_GRANULE), (short)0, MP3G_TIMING_NOLOAD ? 0 : nbytes,
+      const_cast<int16_t*>(coef + (size_t)g * MP3G_COEF_PER_GRANULE), (short)0, nbytes,
       0x00020000);
   const int off = (lane >> 5) * 1152 + (lane & 31) * 36;
 #pragma unroll
@@ -181,7 +173,7 @@ constexpr int kNoRecord = 0x40000000;
 __device__ __forceinline__ void load_lines_lim(const int16_t* coef, uint32_t g, int lane, uint32_t cw[9], int nbytes,
                                                int lim) {
   const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<int16_t*>(coef + (size_t)g * MP3G_COEF_PER_GRANULE), (short)0, MP3G_TIMING_NOLOAD ? 0 : nbytes,
+      const_cast<int16_t*>(coef + (size_t)g * MP3G_COEF_PER_GRANULE), (short)0, nbytes,
       0x00020000);
   const int l0 = 18 * (lane & 31);
   const int off = (lane >> 5) * 1152 + 2 * l0;
@@ -859,7 +851,7 @@ __device__ __forceinline__ void pack_pcm(const f2 acc2[9], int nch, uint32_t pk[
 // with no records (straight-line vmcnt accounting).
 __device__ __forceinline__ void store_pcm(int16_t* pcm, uint32_t g, bool out, const uint32_t pk[9], int hi, int k) {
   const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
-      pcm + (size_t)g * 1152, (short)0, out && !MP3G_TIMING_NOSTORE ? MP3G_PCM_BYTES_PER_GRANULE : 0, 0x00020000);
+      pcm + (size_t)g * 1152, (short)0, out ? MP3G_PCM_BYTES_PER_GRANULE : 0, 0x00020000);
 #pragma unroll
   for (int p = 0; p < 9; p++)
     __builtin_amdgcn_raw_buffer_store_b32(pk[p], rp, 4 * (32 * (2 * p + hi) + k), 0, MP3G_PCM_STORE_AUX);
@@ -898,11 +890,12 @@ __device__ __forceinline__ void load_granule(const mp3g_granule* gran, const int
 
 // Does replayed granule g (< out_from) produce V a later granule reads? Only
 // the last replayed one, or one followed by a granule with fewer channels
-// (see v2 / DESIGN.md halo).
-__device__ __forceinline__ bool replay_needs_v(const mp3g_granule* gran, uint32_t g, uint32_t out_from,
-                                               const WaveSmem& s) {
+// (see v2 / DESIGN.md halo).  Both channel counts come from the headers in
+// memory: it is called before exact_granule has loaded g's descriptor into
+// s.desc, which still holds whatever granule the wave handled last.
+__device__ __forceinline__ bool replay_needs_v(const mp3g_granule* gran, uint32_t g, uint32_t out_from) {
   if (g >= out_from || g + 1 >= out_from) return true;
-  return hdr_nch(gran[g + 1].header) < hdr_nch(s.desc.header);
+  return hdr_nch(gran[g + 1].header) < hdr_nch(gran[g].header);
 }
 
 // One granule in the reference's operation order (the hot-zone fixup):
@@ -1141,7 +1134,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     }
     {
       const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
-          pcm + (size_t)g * 1152, (short)0, out && !MP3G_TIMING_NOSTORE ? MP3G_PCM_BYTES_PER_GRANULE : 0, 0x00020000);
+          pcm + (size_t)g * 1152, (short)0, out ? MP3G_PCM_BYTES_PER_GRANULE : 0, 0x00020000);
 #pragma unroll
       for (int p = 0; p < 9; p++)
         __builtin_amdgcn_raw_buffer_store_b32(pk[p], rp, 4 * (32 * (2 * p + hi) + k), 0, 2);  // non-temporal: c2 -1.9 %, c3 -0.8 %
@@ -1637,7 +1630,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
         have = true;
       }
       for (; gz < ze; gz++) {
-        const bool nv = replay_needs_v(gran, gz, zs, s);
+        const bool nv = replay_needs_v(gran, gz, zs);
         if (exact_granule(gran, coef, pcm, s, sh, gz, gz >= zs, nv, zst)) ze = gz + 2 > ze ? (gz + 2 < end ? gz + 2 : end) : ze;
       }
       done = gz;

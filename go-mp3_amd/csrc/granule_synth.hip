@@ -32,12 +32,6 @@ namespace mp3g {
 namespace v3 {
 
 constexpr int kSynthWaves = 8;
-// MP3G_SYNTH_ABL (diagnostic builds only, wrong PCM): leave out LDS access
-// groups to read SQ_LDS_BANK_CONFLICT per group (tools/gpu_synthlds.sh):
-// 1 staging writes, 2 matrixing, 4 window reads, 8 history shift
-#ifndef MP3G_SYNTH_ABL
-#define MP3G_SYNTH_ABL 0
-#endif
 
 
 // Ping-pong ring: 36 slots per column (stride 38), two halves of 18.  A granule's 18
@@ -80,7 +74,7 @@ __device__ __forceinline__ int synth_pair_line(int lane, int i) {
 }
 __device__ __forceinline__ void synth_load(const float* lines, uint32_t g, uint32_t nbytes, int lane, f2 v[9]) {
   const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float*>(lines + (size_t)g * MP3G_COEF_PER_GRANULE), (short)0, MP3G_TIMING_NOLOAD ? 0 : (int)nbytes,
+      const_cast<float*>(lines + (size_t)g * MP3G_COEF_PER_GRANULE), (short)0, (int)nbytes,
       0x00020000);
   // non-temporal (cache policy nt): the lines are read once; c3 3.21 -> 3.13 ms
   // (the fused kernel's coefficient loads measured +0.9 % with it,
@@ -275,7 +269,7 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
 #if MP3G_HOT_CHECK
     const bool hot1 = __builtin_amdgcn_ballot_w64(max_abs_pairs(buf) > kHotS) != 0;
 #endif
-    if (!(MP3G_SYNTH_ABL & 1)) synth_stage<cur>(s, buf, nch);
+    synth_stage<cur>(s, buf, nch);
     // a later granule in flight during the matrixing and window
     load(gn, buf);
     // a mono granule leaves channel 1 alone (Decode touches ch < nch): its
@@ -294,7 +288,7 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
     // ---- matrixing (frame.go:642-648): lane (ch, slot) turns its S row into X ----
     {
       const int slot = lane & 31;
-      if (!(MP3G_SYNTH_ABL & 2) && ch < nch && slot < 18) {
+      if (ch < nch && slot < 18) {
         float* colu = &s.ring[ch][0][cur + slot];
         dct32::f2 sp[16];
 #pragma unroll
@@ -311,7 +305,7 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
     //      Operands by virtual slot z (see SynthWaveSmem): A = the pair
     //      (z, z + 1), z = 16 + v even (8-B aligned in both layouts), B = z - 1
     //      and z (two dwords; in layout 1 the pair (15, 16) wraps) ----
-    if (out && !(MP3G_SYNTH_ABL & 4)) {
+    if (out) {
       const f2* RA = reinterpret_cast<const f2*>(&s.ring[ch][pa][0]);
       const float* RB = &s.ring[ch][pb][0];
       f2 acc2[9];

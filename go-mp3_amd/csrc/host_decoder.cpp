@@ -39,6 +39,7 @@ int to_status(St s) {
     case St::kEof: return MP3G_EOF;
     case St::kErr: return MP3G_ERR_PARSE;
     case St::kPanic: return MP3G_ERR_UNSUPPORTED;
+    case St::kRead: return MP3G_ERR_READ;
   }
   return MP3G_ERR_PARSE;
 }
@@ -79,6 +80,21 @@ std::mutex g_pin_mu;
 std::vector<PinnedBlock> g_pin_pool;
 constexpr size_t kPinPoolMax = 8;
 
+void pin_free(const PinnedBlock& b);
+
+// Frees every idle pooled pinned block (an allocation failed: the pool's idle
+// memory goes back before the caller is told it is out of memory).  Returns
+// whether anything was freed.
+bool pin_drain() {
+  std::vector<PinnedBlock> v;
+  {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    v.swap(g_pin_pool);
+  }
+  for (const PinnedBlock& b : v) pin_free(b);
+  return !v.empty();
+}
+
 PinnedBlock pin_take(size_t need) {
   {
     std::lock_guard<std::mutex> lk(g_pin_mu);
@@ -93,7 +109,8 @@ PinnedBlock pin_take(size_t need) {
     }
   }
   void* q = nullptr;
-  const bool pin = hipHostMalloc(&q, need, hipHostMallocDefault) == hipSuccess;
+  bool pin = hipHostMalloc(&q, need, hipHostMallocDefault) == hipSuccess;
+  if (!pin && pin_drain()) pin = hipHostMalloc(&q, need, hipHostMallocDefault) == hipSuccess;
   if (!pin) q = std::malloc(need);
   return {static_cast<uint8_t*>(q), q ? need : 0, pin};
 }
@@ -145,7 +162,25 @@ DevBlock dev_take(int device, size_t need) {
     }
   }
   void* q = nullptr;
-  if (hipMalloc(&q, need) != hipSuccess) return {nullptr, 0, device};
+  if (hipMalloc(&q, need) != hipSuccess) {
+    // idle pooled blocks of this device (too small, or merely unused) may be
+    // what the allocation lacks: free them and try once more
+    std::vector<DevBlock> idle;
+    {
+      std::lock_guard<std::mutex> lk(g_pin_mu);
+      for (size_t i = 0; i < g_dev_pool.size();)
+        if (g_dev_pool[i].device == device) {
+          idle.push_back(g_dev_pool[i]);
+          g_dev_pool.erase(g_dev_pool.begin() + i);
+        } else {
+          i++;
+        }
+    }
+    if (idle.empty()) return {nullptr, 0, device};
+    for (const DevBlock& b : idle) (void)hipFree(b.p);  // the caller has `device` current
+    q = nullptr;
+    if (hipMalloc(&q, need) != hipSuccess) return {nullptr, 0, device};
+  }
   return {q, need, device};
 }
 
@@ -262,6 +297,7 @@ struct Batch {
 // ---------------------------------------------------------------------------
 struct mp3g_decoder {
   std::vector<uint8_t> data;  // own copy: no caller pointer is retained
+  mp3g_reader reader{};       // streaming input (mp3g_decoder_new_reader): src.rd points here
   host::Source src;
   host::FrameParser parser;    // MP3G_FLAG_HOST_HUFFMAN: full host parse
   host::FrameScanner scanner;  // default: host scan + GPU main-data kernel
@@ -363,8 +399,12 @@ struct mp3g_decoder {
 
   // Scans (or parses) up to `max_frames` frames into b.  A failing frame ends
   // the batch: b.err, the reservoir is dropped and the next batch starts from
-  // zero DSP state (d.frame = nil after a failed frame.Read).
-  void scan_batch(Batch& b, size_t max_frames) {
+  // zero DSP state (d.frame = nil after a failed frame.Read).  `must`: the
+  // batch is the one Read serves next, so a streaming source without a
+  // seeker may be read (it may block) until it holds one frame; otherwise
+  // such a source contributes only the frames that have fully arrived, and
+  // the batch may come out empty with b.err == MP3G_OK (host::scan_some).
+  void scan_batch(Batch& b, size_t max_frames, bool must) {
     const auto t0 = std::chrono::steady_clock::now();
     struct Acc {
       double& t;
@@ -373,7 +413,7 @@ struct mp3g_decoder {
     } acc{t_scan, t0};
     b.clear();
     b.fresh = scan_fresh;
-    St st = St::kOk;
+    St st;
     if (gpu_huffman()) {
       // drop main data no later frame can reach (the reservoir is < 2 KB)
       const int64_t dead = scanner.live_start(md);
@@ -381,37 +421,40 @@ struct mp3g_decoder {
         md.erase(md.begin(), md.begin() + dead);
         scanner.drop(dead);
       }
-      host::ScannedFrame f;
-      for (size_t i = 0; i < max_frames; i++) {
-        st = scanner.next(src, &f, &md);
-        if (st != St::kOk) break;
+      st = host::scan_some(src, scanner, &md, max_frames, must, [](void* ctx, const host::ScannedFrame& f, int64_t sp) {
+        Batch& b = *static_cast<Batch*>(ctx);
         for (int gr = 0; gr < f.n_granules; gr++) {
           b.gran.push_back(f.gran[gr]);
           b.jobs.push_back(f.job[gr][0]);
           b.jobs.push_back(f.job[gr][1]);
         }
         b.frame_pcm_bytes.push_back((uint32_t)(f.n_granules * MP3G_PCM_BYTES_PER_GRANULE));
-        b.frame_src.push_back(src.pos);
-      }
+        b.frame_src.push_back(sp);
+      }, &b);
       if (!b.gran.empty()) b.md.assign(md.begin(), md.end());  // the scanner keeps editing md
     } else {
-      host::ParsedFrame f;
-      for (size_t i = 0; i < max_frames; i++) {
-        st = parser.next(src, &f);
-        if (st != St::kOk) break;
+      st = host::parse_some(src, parser, max_frames, must, [](void* ctx, const host::ParsedFrame& f, int64_t sp) {
+        Batch& b = *static_cast<Batch*>(ctx);
         for (int gr = 0; gr < f.n_granules; gr++) {
           b.gran.push_back(f.gran[gr]);
           b.coef.insert(b.coef.end(), f.coef[gr], f.coef[gr] + MP3G_COEF_PER_GRANULE);
         }
         b.frame_pcm_bytes.push_back((uint32_t)(f.n_granules * MP3G_PCM_BYTES_PER_GRANULE));
-        b.frame_src.push_back(src.pos);
-      }
+        b.frame_src.push_back(sp);
+      }, &b);
     }
     b.err = st == St::kOk ? MP3G_OK : to_status(st);
-    if (b.err != MP3G_OK) reset_reservoir();
-    scan_fresh = b.gran.empty() || b.err != MP3G_OK;
-    batch_frames = std::min<size_t>(batch_frames * 2, kMaxBatchFrames);
+    if (b.err != MP3G_OK) {
+      reset_reservoir();
+      scan_fresh = true;
+    } else if (!b.gran.empty()) {
+      scan_fresh = false;
+    }  // (an empty batch that has not arrived yet changes nothing)
+    if (!b.gran.empty()) batch_frames = std::min<size_t>(batch_frames * 2, kMaxBatchFrames);
   }
+
+  // A scanned batch worth keeping for the next refill: frames, or a status.
+  static bool has_news(const Batch& b) { return b.n() > 0 || b.err != MP3G_OK; }
 
   void reset_reservoir() {
     parser.reset();
@@ -569,7 +612,7 @@ struct mp3g_decoder {
       inflight = false;
     } else {
       served = scanned ? sc : fl;
-      if (!scanned) scan_batch(bat[served], batch_frames);
+      if (!scanned) scan_batch(bat[served], batch_frames, true);
       scanned = false;
       Batch& b = bat[served];
       if (b.n() == 0) return b.err == MP3G_OK ? MP3G_EOF : b.err;
@@ -585,11 +628,13 @@ struct mp3g_decoder {
     }
     // read ahead: the scanned batch (or a fresh scan) goes on the device...
     const int other = served ^ 1;
-    if (!scanned) scan_batch(bat[other], batch_frames);
+    if (!scanned) scan_batch(bat[other], batch_frames, false);
     scanned = false;
     Batch& nb = bat[other];
     if (nb.n() == 0) {
-      scanned = true;  // only a status: returned by the refill that would serve it
+      // only a status, returned by the refill that would serve it -- or
+      // nothing that has arrived yet (streaming), scanned again by that refill
+      scanned = nb.err != MP3G_OK;
       sc = other;
       return MP3G_OK;
     }
@@ -599,11 +644,19 @@ struct mp3g_decoder {
     fl = other;
     // ...and the one after it is scanned while the device decodes
     if (nb.err == MP3G_OK) {
-      scan_batch(bat[served], batch_frames);
-      scanned = true;
+      scan_batch(bat[served], batch_frames, false);
+      scanned = has_news(bat[served]);
       sc = served;
     }
     return MP3G_OK;
+  }
+
+  // A status of a source operation outside scan_some: a reader error is the
+  // reader's, whatever the short read looked like (decode.go:48-63).
+  int read_status(St st) {
+    const bool failed = src.read_failed;
+    src.read_failed = false;
+    return failed ? MP3G_ERR_READ : to_status(st);
   }
 
   // ensureFrameStartsAndLength (decode.go:154-216)
@@ -614,14 +667,15 @@ struct mp3g_decoder {
     src.seek(0, 0, nullptr);  // rewind
     src.pos = 0;
     St st = src.skip_tags();
-    if (st != St::kOk) return to_status(st);
+    if (st != St::kOk) return read_status(st);
     int64_t l = 0;
     for (;;) {
       uint32_t h;
       int64_t p = src.pos;
+      src.keep_from = src.rpos;  // (reader mode: the walk needs no window behind it)
       st = host::read_header(src, &p, &h);
-      if (st == St::kEof) break;
-      if (st != St::kOk) return to_status(st);
+      if (st == St::kEof && !src.read_failed) break;
+      if (st != St::kOk) return read_status(st);
       frame_starts.push_back(p);
       bytes_per_frame = host::header_bytes_per_frame(h);
       l += bytes_per_frame;
@@ -705,24 +759,11 @@ int mp3g_parse_streams(uint32_t n_streams, const uint8_t* const* datas, const si
 
 void mp3g_free(void* p) { std::free(p); }
 
-int mp3g_decoder_new(const uint8_t* data, size_t len, int seekable, int device, uint32_t mode,
-                     mp3g_decoder** out) {
-  if (!out || (len && !data)) return abi_fail(MP3G_ERR_INVALID_ARGUMENT, "null argument");
-  *out = nullptr;
-  int ndev = 0;
-  if (mp3g_device_count(&ndev) != MP3G_OK || device < 0 || device >= ndev)
-    return abi_fail(MP3G_ERR_NO_DEVICE, "no gfx950 device for the decoder");
-  mp3g_decoder* d = new (std::nothrow) mp3g_decoder;
-  if (!d) return abi_fail(MP3G_ERR_OUT_OF_MEMORY, "decoder");
-  d->data.assign(data, data + len);
-  d->src.data = d->data.data();
-  d->src.len = (int64_t)len;
-  d->src.seekable = seekable != 0;
-  d->device = device;
-  d->mode = mode;
-  // NewDecoder (decode.go:361-388): skip tags, read (here: read ahead from)
-  // the first frame, take the sample rate, scan frame starts + length
-  int rc = to_status(d->src.skip_tags());
+// NewDecoder (decode.go:361-388) on a prepared source: skip tags, read (here:
+// read ahead from) the first frame, take the sample rate, scan frame starts +
+// length (seekers only).
+static int decoder_start(mp3g_decoder* d, mp3g_decoder** out) {
+  int rc = d->read_status(d->src.skip_tags());
   if (rc == MP3G_OK) rc = d->refill();
   if (rc == MP3G_OK) {
     d->sample_rate = host::header_sample_rate(d->first_header);
@@ -734,6 +775,49 @@ int mp3g_decoder_new(const uint8_t* data, size_t len, int seekable, int device, 
   }
   *out = d;
   return MP3G_OK;
+}
+
+static mp3g_decoder* decoder_alloc(int device, uint32_t mode, int* rc) {
+  int ndev = 0;
+  if (mp3g_device_count(&ndev) != MP3G_OK || device < 0 || device >= ndev) {
+    *rc = abi_fail(MP3G_ERR_NO_DEVICE, "no gfx950 device for the decoder");
+    return nullptr;
+  }
+  mp3g_decoder* d = new (std::nothrow) mp3g_decoder;
+  if (!d) {
+    *rc = abi_fail(MP3G_ERR_OUT_OF_MEMORY, "decoder");
+    return nullptr;
+  }
+  d->device = device;
+  d->mode = mode;
+  *rc = MP3G_OK;
+  return d;
+}
+
+int mp3g_decoder_new(const uint8_t* data, size_t len, int seekable, int device, uint32_t mode,
+                     mp3g_decoder** out) {
+  if (!out || (len && !data)) return abi_fail(MP3G_ERR_INVALID_ARGUMENT, "null argument");
+  *out = nullptr;
+  int rc;
+  mp3g_decoder* d = decoder_alloc(device, mode, &rc);
+  if (!d) return rc;
+  d->data.assign(data, data + len);
+  d->src.data = d->data.data();
+  d->src.len = (int64_t)len;
+  d->src.seekable = seekable != 0;
+  return decoder_start(d, out);
+}
+
+int mp3g_decoder_new_reader(const mp3g_reader* reader, int device, uint32_t mode, mp3g_decoder** out) {
+  if (!out || !reader || !reader->read) return abi_fail(MP3G_ERR_INVALID_ARGUMENT, "null argument");
+  *out = nullptr;
+  int rc;
+  mp3g_decoder* d = decoder_alloc(device, mode, &rc);
+  if (!d) return rc;
+  d->reader = *reader;
+  d->src.rd = &d->reader;
+  d->src.seekable = reader->seek != nullptr;
+  return decoder_start(d, out);
 }
 
 void mp3g_decoder_free(mp3g_decoder* d) { delete d; }

@@ -3,6 +3,7 @@
 // buffer and batched output.
 #include "host_parse.h"
 
+#include <algorithm>
 #include <cstring>
 #include <mutex>
 
@@ -420,6 +421,31 @@ St scale_factors_mpeg1(Bits& m, uint32_t h, SideInfo* si, MainData* md, int16_t 
 }  // namespace
 
 // ---- source.go ----------------------------------------------------------------
+bool Source::fill(int64_t end) {  // reader mode: io.Reader.Read into the window
+  if (!may_fetch) {
+    starved = true;
+    return false;
+  }
+  // drop what no rollback or read can reach any more
+  const int64_t drop = std::min(keep_from, rpos) - base;
+  if (drop > 0 && drop >= (int64_t)(win.size() / 2)) {
+    win.erase(win.begin(), win.begin() + drop);
+    base += drop;
+  }
+  const int64_t have_end = base + (int64_t)win.size();
+  const size_t want = std::max<size_t>(fetch_bytes, end > have_end ? (size_t)(end - have_end) : 0);
+  const size_t old = win.size();
+  win.resize(old + want);
+  const int64_t r = rd->read(rd->user, win.data() + old, want);
+  if (r <= 0) {
+    win.resize(old);
+    if (r < 0) read_failed = true;
+    return false;
+  }
+  win.resize(old + (size_t)std::min<int64_t>(r, (int64_t)want));
+  return true;
+}
+
 int64_t Source::read_full(uint8_t* buf, int64_t n, bool* short_read) {  // source.go:99-122
   int64_t got = 0;
   *short_read = false;
@@ -431,9 +457,22 @@ int64_t Source::read_full(uint8_t* buf, int64_t n, bool* short_read) {  // sourc
     got = k;
     if (got == n) return got;
   }
+  const int64_t want = n - got;
+  if (rd) {
+    // io.ReadFull on the reader: Read until n bytes, EOF or an error
+    while (base + (int64_t)win.size() < rpos + want && fill(rpos + want)) {
+    }
+    int64_t avail = base + (int64_t)win.size() - rpos;
+    if (avail < 0) avail = 0;
+    const int64_t k = want < avail ? want : avail;
+    if (k > 0) std::memcpy(buf + got, win.data() + (rpos - base), (size_t)k);
+    rpos += k;
+    pos += k;
+    if (k < want) *short_read = true;
+    return got + k;
+  }
   int64_t avail = len - rpos;
   if (avail < 0) avail = 0;
-  const int64_t want = n - got;
   const int64_t k = want < avail ? want : avail;
   if (k > 0) std::memcpy(buf + got, data + rpos, (size_t)k);
   rpos += k;
@@ -451,6 +490,28 @@ void Source::unread_bytes(const uint8_t* b, int n) {  // source.go:94-97
 
 bool Source::seek(int64_t off, int whence, int64_t* res) {  // source.go:28-40
   if (!seekable) return false;
+  if (rd) {
+    int64_t a;
+    if (whence == 2) {  // the end is the reader's to know
+      a = rd->seek(rd->user, off, 2);
+      if (a < 0) return false;
+      base = a;
+      win.clear();
+    } else {
+      a = whence == 0 ? off : rpos + off;
+      if (a < 0) return false;
+      if (a < base || a > base + (int64_t)win.size()) {
+        a = rd->seek(rd->user, a, 0);
+        if (a < 0) return false;
+        base = a;
+        win.clear();
+      }
+    }
+    n_unread = 0;
+    rpos = pos = a;
+    if (res) *res = a;
+    return true;
+  }
   n_unread = 0;
   const int64_t a = whence == 0 ? off : whence == 1 ? rpos + off : len + off;
   if (a < 0) return false;
@@ -458,6 +519,22 @@ bool Source::seek(int64_t off, int whence, int64_t* res) {  // source.go:28-40
   pos = a;
   if (res) *res = a;
   return true;
+}
+
+Source::Mark Source::mark() const {
+  Mark m;
+  m.rpos = rpos;
+  m.pos = pos;
+  m.n_unread = n_unread;
+  std::memcpy(m.unread, unread, sizeof unread);
+  return m;
+}
+
+void Source::restore(const Mark& m) {
+  rpos = m.rpos;
+  pos = m.pos;
+  n_unread = m.n_unread;
+  std::memcpy(unread, m.unread, sizeof unread);
 }
 
 St Source::skip_tags() {  // source.go:42-83
@@ -479,6 +556,16 @@ St Source::skip_tags() {  // source.go:42-83
       if (n != 4) return St::kOk;
       const int64_t size = ((int64_t)tmp[0] << 21) | ((int64_t)tmp[1] << 14) | ((int64_t)tmp[2] << 7) | tmp[3];
       // skip `size` bytes (io.ReadFull into a scratch buffer)
+      if (rd) {
+        uint8_t scratch[4096];
+        for (int64_t left = size; left > 0;) {
+          const int64_t k = left < (int64_t)sizeof scratch ? left : (int64_t)sizeof scratch;
+          left -= read_full(scratch, k, &sr);
+          if (sr) return St::kEof;
+          keep_from = rpos;  // the tag's bytes are never read again
+        }
+        continue;
+      }
       const int64_t avail = n_unread + (len - rpos > 0 ? len - rpos : 0);
       const int64_t k = size < avail ? size : avail;
       int64_t left = k;
@@ -809,6 +896,50 @@ St FrameScanner::next_impl(Source& s, ScannedFrame* out, Md* md) {
   prev_start_ = vstart;
   have_prev_ = true;
   return St::kOk;
+}
+
+// ---- the decoder's read-ahead step (decode.go:45-67 repeated) -----------------
+namespace {
+template <class Next, class Emit>
+St scan_frames(Source& src, size_t max_frames, bool must, Next next, Emit emit) {
+  const bool eager = !src.rd || src.seekable;
+  St st = St::kOk;
+  for (size_t i = 0; i < max_frames; i++) {
+    src.may_fetch = eager || (must && i == 0);
+    src.starved = false;
+    src.keep_from = src.rpos;
+    const Source::Mark m = src.mark();
+    st = next();
+    if (st != St::kOk) {
+      if (src.starved) {  // not all of it has arrived: leave it for a later call
+        src.restore(m);
+        st = St::kOk;
+      } else if (src.read_failed) {
+        st = St::kRead;
+      }
+      break;
+    }
+    emit();
+  }
+  src.may_fetch = true;
+  src.starved = false;
+  src.read_failed = false;
+  return st;
+}
+}  // namespace
+
+St scan_some(Source& src, FrameScanner& sc, std::vector<uint8_t>* md, size_t max_frames, bool must,
+             void (*emit)(void* ctx, const ScannedFrame& f, int64_t src_pos), void* ctx) {
+  ScannedFrame f;
+  return scan_frames(
+      src, max_frames, must, [&] { return sc.next(src, &f, md); }, [&] { emit(ctx, f, src.pos); });
+}
+
+St parse_some(Source& src, FrameParser& fp, size_t max_frames, bool must,
+              void (*emit)(void* ctx, const ParsedFrame& f, int64_t src_pos), void* ctx) {
+  ParsedFrame f;
+  return scan_frames(
+      src, max_frames, must, [&] { return fp.next(src, &f); }, [&] { emit(ctx, f, src.pos); });
 }
 
 }  // namespace host

@@ -21,10 +21,21 @@
 namespace mp3g {
 namespace host {
 
-// Error classes the reference's decode.go distinguishes.
-enum class St { kOk = 0, kEof = 1, kErr = 2, kPanic = 3 };
+// Error classes the reference's decode.go distinguishes.  kRead: the
+// caller's io.Reader failed (decode.go:48-63 passes its error through).
+enum class St { kOk = 0, kEof = 1, kErr = 2, kPanic = 3, kRead = 4 };
 
-// source.go over an in-memory bytes.Reader (seekable = implements io.Seeker).
+// source.go (source.go:22-122) over one of two byte sources:
+//  * in memory (data, len): a bytes.Reader; seekable = implements io.Seeker;
+//  * reader mode (rd != nullptr): the caller's io.Reader / io.Seeker as
+//    callbacks (mp3g_reader).  Bytes are pulled into a window of the stream,
+//    [base, base + win.size()); rpos is the absolute stream position of the
+//    next byte.  A read past the window calls rd->read (io.Reader.Read: any
+//    count >= 1, 0 = io.EOF, < 0 = error) unless may_fetch is off, in which
+//    case the read stops short and sets `starved` -- the decoder's read-ahead
+//    uses that to scan only bytes that have already arrived (a live stream's
+//    Read may block).  Seeks inside the window move rpos; others go to
+//    rd->seek and empty the window.
 struct Source {
   const uint8_t* data = nullptr;
   int64_t len = 0;
@@ -34,10 +45,33 @@ struct Source {
   int n_unread = 0;
   int64_t pos = 0;  // source.pos
 
+  // ---- reader mode ----
+  const mp3g_reader* rd = nullptr;
+  std::vector<uint8_t> win;
+  int64_t base = 0;
+  int64_t keep_from = 0;   // a fetch may drop window bytes before min(keep_from, rpos)
+  bool may_fetch = true;   // reads past the window may call rd->read
+  bool starved = false;    // a read stopped short because may_fetch was off
+  bool read_failed = false;  // rd->read returned an error (cleared by the caller)
+  size_t fetch_bytes = 64 << 10;  // bytes asked of one rd->read
+
   int64_t read_full(uint8_t* buf, int64_t n, bool* short_read);
   void unread_bytes(const uint8_t* b, int n);
   bool seek(int64_t off, int whence, int64_t* res);
   St skip_tags();
+
+  // Position state for a rollback (reader mode: the window keeps the bytes
+  // from keep_from on, so a restore never needs the reader again).
+  struct Mark {
+    int64_t rpos, pos;
+    int n_unread;
+    uint8_t unread[16];
+  };
+  Mark mark() const;
+  void restore(const Mark& m);
+
+ private:
+  bool fill(int64_t end);  // reader mode: grow the window towards `end`
 };
 
 // One parsed frame: its header, start offset and the boundary input of its
@@ -108,6 +142,21 @@ class FrameScanner {
   template <class Md>
   St next_impl(Source& src, ScannedFrame* out, Md* md);
 };
+
+// One read-ahead step of the decoder (decode.go:45-67 repeated): up to
+// max_frames frames from the source's position, each handed to `emit` with
+// the source position after it.  Returns the status that ended the scan
+// (kOk: max_frames reached, or -- reader mode -- the next frame is not fully
+// buffered and may not be fetched).  Fetch rule: an in-memory or seekable
+// source always reads; a non-seekable reader is read only while `must` is set
+// and no frame has been scanned in this call, i.e. only when the decoder holds
+// no complete frame it has not decoded -- where the reference's Decoder.Read
+// would block too.  A frame cut short by that rule is rolled back: the
+// scanner state, *md and the source position are as before it.
+St scan_some(Source& src, FrameScanner& sc, std::vector<uint8_t>* md, size_t max_frames, bool must,
+             void (*emit)(void* ctx, const ScannedFrame& f, int64_t src_pos), void* ctx);
+St parse_some(Source& src, FrameParser& fp, size_t max_frames, bool must,
+              void (*emit)(void* ctx, const ParsedFrame& f, int64_t src_pos), void* ctx);
 
 // frameheader.Read: sync search from the source position.
 St read_header(Source& s, int64_t* pos_io, uint32_t* out);

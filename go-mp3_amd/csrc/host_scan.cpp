@@ -78,6 +78,7 @@ int to_status(St s) {
     case St::kEof: return MP3G_EOF;
     case St::kErr: return MP3G_ERR_PARSE;
     case St::kPanic: return MP3G_ERR_UNSUPPORTED;
+    case St::kRead: return MP3G_ERR_READ;
   }
   return MP3G_ERR_PARSE;
 }

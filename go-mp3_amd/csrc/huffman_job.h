@@ -328,10 +328,6 @@ MP3G_HD_INLINE int decode_job(const mp3g_hjob& job, uint64_t j, const uint64_t* 
 
   // ---- scale factors ----
   const int slen1 = J.slen[0], slen2 = J.slen[1];
-#ifdef MP3G_EXP_HUFF_NO_SF  // timing experiments only (wrong output)
-  r.seek(part2);
-  if (0)
-#endif
   switch (J.sf_kind) {
     case MP3G_SF_MPEG1_LONG:
       if (J.scfsi) {
@@ -387,11 +383,7 @@ MP3G_HD_INLINE int decode_job(const mp3g_hjob& job, uint64_t j, const uint64_t* 
 
   // ---- Huffman (maindata/huffman.go:27-138) ----
   int i = 0, count1 = 0;
-#ifdef MP3G_EXP_HUFF_NO_BV  // timing experiments only (wrong output)
-  const uint32_t p23 = 0;
-#else
   const uint32_t p23 = J.part2_3_length;
-#endif
   if (p23) {
     const uint32_t pend = part2 + p23 - 1;  // bitPosEnd
     const int bv2 = 2 * (int)J.big_values;  // <= 576 (the scan rejects more)

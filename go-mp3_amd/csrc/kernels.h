@@ -27,10 +27,9 @@ static_assert(sizeof(ChunkDesc) == 32, "ChunkDesc layout");
 
 // Host-side launchers (defined next to the kernels; no RDC needed).
 hipError_t upload_tables(const DspTables& tables);
-// Exact-mode kernel variants: v1 = per-phase reference implementation,
-// v2 = fused/register-blocked workgroup kernel (both kept as cross-checks:
-// MP3G_FLAG_KERNEL_V1 / _V2), v4 = one wave per chunk (default).
-constexpr int kVariantV1 = 1;
+// Exact-mode kernel variants: v2 = fused/register-blocked workgroup kernel
+// (kept as the cross-check: MP3G_FLAG_KERNEL_V2), v4 = one wave per chunk
+// (default).  (v1, the per-phase version, was retired in round 4.)
 constexpr int kVariantV2 = 2;
 // fast mode (MP3G_MODE_FAST): one wave per chunk, reassociated transforms, +-1 LSB
 constexpr int kVariantFast = 3;

@@ -2,9 +2,9 @@
 // kernels of libmp3g.so.
 //
 // Holds their constant tables (uploaded once per device), the workgroup
-// exact-mode kernels v1 (granule_exact.hip, the straightforward per-phase
-// version) and v2 (granule_fused.hip), both kept as on-device cross-checks of
-// the default exact kernel v4 (kernels_fast.hip), and the main-data (scale factor + Huffman) kernel
+// exact-mode kernel v2 (granule_fused.hip), kept as the on-device cross-check
+// of the default exact kernel v4 (kernels_fast.hip; the per-phase v1 was
+// retired in round 4), and the main-data (scale factor + Huffman) kernel
 // (huffman_dev.hip).  One TU so they reach g_tab / g_huff without
 // relocatable device code.  The fast-mode kernel v3 has a TU of its own
 // (kernels_fast.hip: its own table copy g_fast and codegen options).
@@ -24,7 +24,6 @@ __device__ HuffLut g_huff;
 }  // namespace mp3g
 
 #include "granule_common.hip"
-#include "granule_exact.hip"
 #include "granule_fused.hip"
 #include "huffman_dev.hip"
 
@@ -56,9 +55,6 @@ int chunks_per_cu(int variant) {
     e = fast_kernel_attributes(&a, &waves_per_block);
   } else if (variant == kVariantExact4) {
     e = wexact_kernel_attributes(&a, &waves_per_block);
-  } else if (variant == kVariantV1) {
-    e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&v1::granule_exact_kernel));
-    waves_per_block = 4;
   } else {
     e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&v2::granule_fused_kernel));
     waves_per_block = 4;
@@ -83,12 +79,8 @@ hipError_t launch_granule(int variant, const ChunkDesc* d_chunks, uint32_t n_chu
     return launch_fast(d_chunks, n_chunks, d_gran, d_coef, d_state_in, d_state_out, d_pcm, nullptr, stream);
   if (variant == kVariantExact4)
     return launch_wexact(d_chunks, n_chunks, d_gran, d_coef, d_state_in, d_state_out, d_pcm, stream);
-  if (variant == kVariantV1)
-    hipLaunchKernelGGL(v1::granule_exact_kernel, dim3(n_chunks), dim3(256), 0, stream, d_chunks,
-                       d_gran, d_coef, d_state_in, d_state_out, d_pcm);
-  else
-    hipLaunchKernelGGL(v2::granule_fused_kernel, dim3(n_chunks), dim3(256), 0, stream, d_chunks,
-                       d_gran, d_coef, d_state_in, d_state_out, d_pcm);
+  hipLaunchKernelGGL(v2::granule_fused_kernel, dim3(n_chunks), dim3(256), 0, stream, d_chunks,
+                     d_gran, d_coef, d_state_in, d_state_out, d_pcm);
   return hipGetLastError();
 }
 

@@ -92,10 +92,9 @@ int ensure_device(int dev) {
 // faster than one round of 683-granule chunks; sweeps measured on MI355X,
 // tools/gpu_chunks.sh).
 // The granule kernel a plan's mode runs: fast v3, or exact v4 unless a
-// cross-check kernel is asked for (MP3G_FLAG_KERNEL_V1 / _V2).
+// cross-check kernel is asked for (MP3G_FLAG_KERNEL_V2).
 int plan_variant(uint32_t mode) {
   if ((mode & 0xffu) == MP3G_MODE_FAST) return kVariantFast;
-  if (mode & MP3G_FLAG_KERNEL_V1) return kVariantV1;
   if (mode & MP3G_FLAG_KERNEL_V2) return kVariantV2;
   return kVariantExact4;
 }
@@ -202,6 +201,7 @@ const char* mp3g_status_string(int s) {
     case MP3G_ERR_UNSUPPORTED: return "unsupported stream";
     case MP3G_ERR_NO_XING_HEADER: return "lameinfo: no Xing/Info header found";
     case MP3G_ERR_UNEXPECTED_EOF: return "unexpected EOF";
+    case MP3G_ERR_READ: return "reader error";
   }
   return "unknown status";
 }
@@ -269,6 +269,7 @@ int mp3g_plan_create(int device, const mp3g_stream* streams, uint32_t n_streams,
   const uint32_t base_mode = mode & 0xffu;
   if (base_mode != MP3G_MODE_EXACT && base_mode != MP3G_MODE_FAST)
     return fail(MP3G_ERR_UNSUPPORTED, "mode not available");
+  if (mode & MP3G_FLAG_KERNEL_V1) return fail(MP3G_ERR_UNSUPPORTED, "the v1 exact kernel was retired (ABI 3)");
   for (uint32_t s = 0; s < n_streams; s++) {
     // the one-wave kernels (fast v3, exact v4) index granules with 32-bit
     // wave-uniform scalars

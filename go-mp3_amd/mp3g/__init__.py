@@ -45,8 +45,16 @@ MP3G_PCM_BYTES_PER_GRANULE = 2304  # include/mp3g.h: 576 stereo s16 samples
 
 STATUS = {0: "ok", 1: "invalid argument", 2: "invalid granule", 3: "no device", 4: "device error",
           5: "out of memory", 6: "parse error", 7: "eof", 8: "unsupported", 9: "no Xing/Info header",
-          10: "unexpected EOF"}
-ERR_NO_XING_HEADER, ERR_UNEXPECTED_EOF, EOF = 9, 10, 7
+          10: "unexpected EOF", 11: "reader error"}
+ERR_NO_XING_HEADER, ERR_UNEXPECTED_EOF, EOF, ERR_READ = 9, 10, 7, 11
+
+# include/mp3g.h mp3g_reader: io.Reader.Read / io.Seeker.Seek as C callbacks
+READ_FN = C.CFUNCTYPE(C.c_int64, C.c_void_p, C.POINTER(C.c_uint8), C.c_size_t)
+SEEK_FN = C.CFUNCTYPE(C.c_int64, C.c_void_p, C.c_int64, C.c_int)
+
+
+class _Reader(C.Structure):
+    _fields_ = [("read", READ_FN), ("seek", SEEK_FN), ("user", C.c_void_p)]
 
 
 class Mp3gError(RuntimeError):
@@ -111,6 +119,7 @@ def lib():
         L.mp3g_release_cached_buffers.argtypes = []
         L.mp3g_release_cached_buffers.restype = None
         L.mp3g_decoder_new.argtypes = [vp, sz, C.c_int, C.c_int, u32, C.POINTER(vp)]
+        L.mp3g_decoder_new_reader.argtypes = [C.POINTER(_Reader), C.c_int, u32, C.POINTER(vp)]
         L.mp3g_decoder_free.argtypes = [vp]
         L.mp3g_decoder_read.argtypes = [vp, vp, sz, C.POINTER(sz)]
         L.mp3g_decoder_read_full.argtypes = [vp, vp, sz, C.POINTER(sz)]
@@ -432,6 +441,40 @@ class Decoder:
         buf = np.frombuffer(data, dtype=np.uint8) if len(data) else np.zeros(1, np.uint8)
         self._h = C.c_void_p()
         _check(lib().mp3g_decoder_new(_ptr(buf), len(data), int(seekable), device, mode, C.byref(self._h)))
+
+    @classmethod
+    def from_reader(cls, read, seek=None, mode=MODE_EXACT, device=0):
+        """mp3.NewDecoder(r) on a streaming source (mp3g_decoder_new_reader):
+        read(n) -> bytes (io.Reader.Read: 1..n bytes, b"" = io.EOF, an
+        exception = a reader error); seek(offset, whence) -> new offset, or
+        None when the source is no io.Seeker.  Returns once the tags and frame
+        0 are in (non-seekable) -- the decoder pulls the rest as Read needs it."""
+        self = cls.__new__(cls)
+        self._h = C.c_void_p()
+        self.read_errors = []
+
+        def _read(_user, buf, cap):
+            try:
+                b = read(int(cap))
+            except Exception as e:  # a reader error: the decoder returns MP3G_ERR_READ
+                self.read_errors.append(e)
+                return -1
+            k = min(len(b), int(cap))
+            if k:
+                C.memmove(buf, b, k)
+            return k
+
+        def _seek(_user, off, whence):
+            try:
+                return int(seek(int(off), int(whence)))
+            except Exception:
+                return -1
+
+        # the callbacks must outlive the decoder
+        self._cb = (READ_FN(_read), SEEK_FN(_seek) if seek is not None else SEEK_FN())
+        r = _Reader(self._cb[0], self._cb[1], None)
+        _check(lib().mp3g_decoder_new_reader(C.byref(r), device, mode, C.byref(self._h)))
+        return self
 
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:

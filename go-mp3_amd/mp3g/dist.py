@@ -101,12 +101,19 @@ def max_over_ranks(value, device=None):
     return float(t.item())
 
 
-def gather_pcm(pcm, dst=0):
-    """Gather every rank's PCM (1-D int16/uint8 tensor, sizes may differ) to
-    `dst`; returns the concatenation in rank order on dst, None elsewhere.
-    One padded collective: sizes first, then a single gather of max-size
-    buffers (xGMI is point-to-point, so one large transfer per link beats
-    many small ones)."""
+def gather_pcm(pcm, dst=0, out=None):
+    """Gather every rank's PCM (a 1-D tensor of any dtype, sizes may differ) to
+    `dst`: returns `out` -- the concatenation in rank order, as raw bytes
+    viewed as pcm's dtype -- on dst, None elsewhere.
+
+    The sizes go first (one small all_gather); then every other rank sends its
+    PCM point-to-point straight into its slice of ONE output buffer on dst
+    (preallocated by the caller as `out`, or allocated here), and dst copies
+    its own part into place.  No per-rank staging buffers and no concatenation
+    copy: at c4 that is 38.65 GB written once on rank 0.  xGMI
+    is point-to-point, so the world - 1 transfers run concurrently on rank 0's
+    links.  Works on GPU tensors under RCCL and on CPU tensors under gloo.
+    """
     import torch
     import torch.distributed as dist
     world, rank = dist.get_world_size(), dist.get_rank()
@@ -116,11 +123,25 @@ def gather_pcm(pcm, dst=0):
     sizes = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(sizes, n)
     sizes = [int(s.item()) for s in sizes]
-    cap = max(sizes) if sizes else 0
-    buf = torch.zeros(cap, dtype=flat.dtype, device=flat.device)
-    buf[:flat.numel()] = flat
-    bufs = [torch.empty_like(buf) for _ in range(world)] if rank == dst else None
-    dist.gather(buf, bufs, dst=dst)
     if rank != dst:
+        if flat.numel():
+            for req in dist.batch_isend_irecv([dist.P2POp(dist.isend, flat, dst)]):
+                req.wait()
         return None
-    return torch.cat([b[:s] for b, s in zip(bufs, sizes)]).view(dtype)
+    total = sum(sizes)
+    if out is None:
+        out_b = torch.empty(total, dtype=torch.uint8, device=flat.device)
+    else:
+        out_b = out.reshape(-1).view(torch.uint8)
+        if out_b.numel() < total or out_b.device != flat.device:
+            raise ValueError(f"gather_pcm: out holds {out_b.numel()} B on {out_b.device}, "
+                             f"need {total} B on {flat.device}")
+        out_b = out_b[:total]
+    offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    ops = [dist.P2POp(dist.irecv, out_b[int(offs[r]):int(offs[r + 1])], r)
+           for r in range(world) if r != dst and sizes[r]]
+    reqs = dist.batch_isend_irecv(ops) if ops else []
+    out_b[int(offs[dst]):int(offs[dst + 1])].copy_(flat)
+    for req in reqs:
+        req.wait()
+    return out_b.view(dtype) if out is None else out

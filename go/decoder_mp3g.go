@@ -7,7 +7,14 @@
 // the GPU (main data and DSP), carrying the DSP state between batches.
 // Also DecodeMany, the batch API for servers (mp3g_decode_streams).
 //
-// Written from include/mp3g.h (ABI version 2); tests/test_cgo_shim_cpu.py
+// The io.Reader is streamed, not slurped: NewDecoder hands the library two
+// callbacks (reader_mp3g.c trampolines into mp3gGoRead / mp3gGoSeek below),
+// so it returns once the tags and frame 0 are in, as the reference's does
+// (decode.go:361-388), and Read pulls input only as the read-ahead needs it
+// (source.go:99-122) -- a live stream that has not ended gets a decoder and
+// every frame that has arrived.
+//
+// Written from include/mp3g.h (ABI version 3); tests/test_cgo_shim_cpu.py
 // checks every C identifier used here against the header.
 package mp3
 
@@ -15,7 +22,11 @@ package mp3
 #cgo CFLAGS: -I${SRCDIR}/third_party/mp3g/include
 #cgo LDFLAGS: -L${SRCDIR}/third_party/mp3g/lib -lmp3g -Wl,-rpath,${SRCDIR}/third_party/mp3g/lib
 #include <stdlib.h>
+#include <stdint.h>
 #include "mp3g.h"
+// reader_mp3g.c: an mp3g_reader whose callbacks call the exported Go
+// functions below with the cgo.Handle h as the user value
+int goreader_decoder_new(uintptr_t h, int seekable, int device, uint32_t mode, mp3g_decoder** out);
 */
 import "C"
 
@@ -23,6 +34,7 @@ import (
 	"errors"
 	"fmt"
 	"io"
+	"runtime/cgo"
 	"time"
 	"unsafe"
 )
@@ -41,17 +53,85 @@ func statusError(st C.int) error {
 }
 
 // Decoder is a MP3-decoded stream (decode.go:34-43). Not safe for concurrent use.
-type Decoder struct{ d *C.mp3g_decoder }
+type Decoder struct {
+	d  *C.mp3g_decoder
+	h  cgo.Handle   // the reader state the C callbacks reach (0 for NewDecoderBytes)
+	rs *readerState // nil for NewDecoderBytes
+}
 
-// NewDecoder decodes the given io.Reader (decode.go:361-388); the whole
-// stream is read up front and copied by the library (nothing Go-owned is
-// retained across calls).
-func NewDecoder(r io.Reader) (*Decoder, error) {
-	data, err := io.ReadAll(r)
+// readerState is what the library's callbacks reach through the handle: the
+// caller's reader and the error a failed Read / Seek returned, handed back
+// from the decoder call that ran into it (decode.go:48-63 passes a reader's
+// error through).
+type readerState struct {
+	r    io.Reader
+	s    io.Seeker // nil: not an io.Seeker (Length() = -1)
+	err  error     // the reader's last error
+	pend error     // an error Read returned together with data: reported by the next call
+}
+
+//export mp3gGoRead
+func mp3gGoRead(h C.uintptr_t, buf *C.uint8_t, n C.size_t) C.int64_t {
+	rs := cgo.Handle(h).Value().(*readerState)
+	if e := rs.pend; e != nil {
+		rs.pend = nil
+		if e == io.EOF || e == io.ErrUnexpectedEOF {
+			return 0
+		}
+		rs.err = e
+		return -1
+	}
+	p := unsafe.Slice((*byte)(unsafe.Pointer(buf)), int(n))
+	for { // io.ReadFull's loop: (0, nil) asks again
+		k, err := rs.r.Read(p)
+		if k > 0 {
+			rs.pend = err
+			return C.int64_t(k)
+		}
+		if err == io.EOF || err == io.ErrUnexpectedEOF { // source.go:112-118
+			return 0
+		}
+		if err != nil {
+			rs.err = err
+			return -1
+		}
+	}
+}
+
+//export mp3gGoSeek
+func mp3gGoSeek(h C.uintptr_t, off C.int64_t, whence C.int) C.int64_t {
+	rs := cgo.Handle(h).Value().(*readerState)
+	n, err := rs.s.Seek(int64(off), int(whence))
 	if err != nil {
+		rs.err = err
+		return -1
+	}
+	return C.int64_t(n)
+}
+
+// NewDecoder decodes the given io.Reader (decode.go:361-388), streaming it:
+// the library calls back into r as it needs bytes and never retains a Go
+// pointer (the callbacks get a cgo.Handle).
+func NewDecoder(r io.Reader) (*Decoder, error) {
+	rs := &readerState{r: r}
+	seekable := C.int(0)
+	if s, ok := r.(io.Seeker); ok {
+		rs.s = s
+		seekable = 1
+	}
+	h := cgo.NewHandle(rs)
+	var d *C.mp3g_decoder
+	if st := C.goreader_decoder_new(C.uintptr_t(h), seekable, 0, Mode, &d); st != C.MP3G_OK {
+		err := rs.statusError(st)
+		h.Delete()
 		return nil, err
 	}
-	_, seekable := r.(io.Seeker)
+	return &Decoder{d: d, h: h, rs: rs}, nil
+}
+
+// NewDecoderBytes decodes a complete stream already in memory (the library
+// copies it; no callbacks): seekable as for a bytes.Reader.
+func NewDecoderBytes(data []byte, seekable bool) (*Decoder, error) {
 	var p *C.uint8_t
 	if len(data) > 0 {
 		p = (*C.uint8_t)(unsafe.Pointer(&data[0]))
@@ -64,14 +144,28 @@ func NewDecoder(r io.Reader) (*Decoder, error) {
 	if st := C.mp3g_decoder_new(p, C.size_t(len(data)), s, 0, Mode, &d); st != C.MP3G_OK {
 		return nil, statusError(st)
 	}
-	return &Decoder{d}, nil
+	return &Decoder{d: d}, nil
 }
+
+// statusError with the reader's own error for MP3G_ERR_READ.
+func (rs *readerState) statusError(st C.int) error {
+	if st == C.MP3G_ERR_READ && rs != nil && rs.err != nil {
+		return rs.err
+	}
+	return statusError(st)
+}
+
+func (d *Decoder) statusError(st C.int) error { return d.rs.statusError(st) }
 
 // Close releases the decoder's host and device memory.
 func (d *Decoder) Close() error {
 	if d.d != nil {
 		C.mp3g_decoder_free(d.d)
 		d.d = nil
+	}
+	if d.h != 0 {
+		d.h.Delete()
+		d.h = 0
 	}
 	return nil
 }
@@ -84,7 +178,7 @@ func (d *Decoder) Read(buf []byte) (int, error) {
 	var n C.size_t
 	st := C.mp3g_decoder_read(d.d, (*C.uint8_t)(unsafe.Pointer(&buf[0])), C.size_t(len(buf)), &n)
 	if st != C.MP3G_OK {
-		return int(n), statusError(st)
+		return int(n), d.statusError(st)
 	}
 	return int(n), nil
 }
@@ -104,14 +198,14 @@ func (d *Decoder) ReadFull(buf []byte) (int, error) {
 	case st == C.MP3G_EOF:
 		return int(n), io.ErrUnexpectedEOF
 	}
-	return int(n), statusError(st)
+	return int(n), d.statusError(st)
 }
 
 // Seek is io.Seeker's Seek (decode.go:89-145), with the reference's warm-up.
 func (d *Decoder) Seek(offset int64, whence int) (int64, error) {
 	var np C.int64_t
 	if st := C.mp3g_decoder_seek(d.d, C.int64_t(offset), C.int(whence), &np); st != C.MP3G_OK {
-		return 0, statusError(st)
+		return 0, d.statusError(st)
 	}
 	return int64(np), nil
 }
@@ -143,13 +237,13 @@ func (d *Decoder) Progress() float64     { return float64(C.mp3g_decoder_progres
 func (d *Decoder) SamplePosition() int64 { return int64(C.mp3g_decoder_sample_position(d.d)) }
 func (d *Decoder) SampleCount() int64    { return int64(C.mp3g_decoder_sample_count(d.d)) }
 func (d *Decoder) SeekToSample(s int64) error {
-	return statusError(C.mp3g_decoder_seek_to_sample(d.d, C.int64_t(s)))
+	return d.statusError(C.mp3g_decoder_seek_to_sample(d.d, C.int64_t(s)))
 }
 func (d *Decoder) SeekToTime(t time.Duration) error {
-	return statusError(C.mp3g_decoder_seek_to_time_ns(d.d, C.int64_t(t)))
+	return d.statusError(C.mp3g_decoder_seek_to_time_ns(d.d, C.int64_t(t)))
 }
 func (d *Decoder) Skip(dt time.Duration) error {
-	return statusError(C.mp3g_decoder_skip_ns(d.d, C.int64_t(dt)))
+	return d.statusError(C.mp3g_decoder_skip_ns(d.d, C.int64_t(dt)))
 }
 
 // DecodeMany decodes complete MP3 files on the GPU, the main data included:

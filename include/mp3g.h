@@ -32,8 +32,10 @@ extern "C" {
 
 /* 2: mp3g_lame_toc_offset returns a status and writes the offset through an
  *    out-parameter (version 1 returned the offset); the fast-mode hot-granule
- *    fallback (no signature change). */
-#define MP3G_ABI_VERSION 2
+ *    fallback (no signature change).
+ * 3: streaming input -- mp3g_reader + mp3g_decoder_new_reader, MP3G_ERR_READ;
+ *    MP3G_FLAG_KERNEL_V1 retired. */
+#define MP3G_ABI_VERSION 3
 
 /* ---- status codes ------------------------------------------------------ */
 typedef enum mp3g_status {
@@ -47,7 +49,9 @@ typedef enum mp3g_status {
   MP3G_EOF = 7,                  /* end of stream (decoder API, io.EOF)      */
   MP3G_ERR_UNSUPPORTED = 8,      /* MPEG 2.5, layer I/II, free format, ...   */
   MP3G_ERR_NO_XING_HEADER = 9,   /* lameinfo.ErrNoXingHeader                 */
-  MP3G_ERR_UNEXPECTED_EOF = 10   /* io.ErrUnexpectedEOF (lameinfo.ParseFromReader) */
+  MP3G_ERR_UNEXPECTED_EOF = 10, /* io.ErrUnexpectedEOF (lameinfo.ParseFromReader) */
+  MP3G_ERR_READ = 11             /* the caller's reader callback failed (decoder API;
+                                    decode.go:48-63 returns a reader's error as is) */
 } mp3g_status;
 
 /* ---- boundary input: one granule descriptor ---------------------------- */
@@ -104,7 +108,7 @@ typedef struct mp3g_granule {
  * decoder produced (Frame.store / vVec are only ever written by Decode): its
  * vVec blocks are V = synthNWin * S, whose 64 entries hold 33 distinct values,
  * and the one-wave kernels (fast v3, exact v4) keep only those; the workgroup
- * kernels (MP3G_FLAG_KERNEL_V1 / _V2) carry all 64 of any vvec. */
+ * kernel (MP3G_FLAG_KERNEL_V2) carries all 64 of any vvec. */
 typedef struct mp3g_state {
   float store[2][32][18]; /* IMDCT overlap                          */
   float vvec[2][1024];    /* polyphase FIFO, newest V block at [0:64] */
@@ -128,7 +132,8 @@ typedef struct mp3g_stream {
 #define MP3G_MODE_EXACT 0u   /* bit-exact vs the reference (linux/amd64 float semantics) */
 #define MP3G_MODE_FAST  1u   /* reassociated fast transforms; |dPCM| <= 1 LSB            */
 #define MP3G_FLAG_CHECKED 0x100u /* validate descriptor ranges on the host first      */
-#define MP3G_FLAG_KERNEL_V1 0x200u /* exact mode via the per-phase v1 kernel (cross-check) */
+#define MP3G_FLAG_KERNEL_V1 0x200u /* retired in ABI 3 (the per-phase v1 cross-check kernel):
+                                      mp3g_plan_create returns MP3G_ERR_UNSUPPORTED */
 #define MP3G_FLAG_KERNEL_V2 0x800u /* exact mode via the workgroup v2 kernel (cross-check; the
                                       default exact kernel is v4, one wave per chunk) */
 #define MP3G_FLAG_HOST_HUFFMAN 0x400u /* decoder: scale factors + Huffman on the host (mp3g_parse_*)
@@ -285,7 +290,7 @@ int mp3g_huffman_execute(int device, const mp3g_hjob* d_jobs, uint64_t n_granule
 /* The same with flags.  MP3G_HUFF_ROWS_COUNT1: each coefficient row is
  * written only up to its count1 plus padding (the zero tail is left as it
  * was): what the default plan kernels (MP3G_MODE_FAST, and MP3G_MODE_EXACT
- * without MP3G_FLAG_KERNEL_V1 / _V2) read, since lines at and above count1
+ * without MP3G_FLAG_KERNEL_V2) read, since lines at and above count1
  * are zero (maindata/huffman.go:127-134).  The batch and decoder APIs use it
  * for those modes (c3 main-data kernel -13 %). */
 #define MP3G_HUFF_ROWS_COUNT1 1u
@@ -331,6 +336,34 @@ void mp3g_release_cached_buffers(void);
 typedef struct mp3g_decoder mp3g_decoder;
 int mp3g_decoder_new(const uint8_t* data, size_t len, int seekable, int device, uint32_t mode,
                      mp3g_decoder** out);
+
+/* Streaming input: the caller's io.Reader (and io.Seeker) as callbacks, so a
+ * decoder runs on input it has not got yet -- a pipe, a socket, a live radio
+ * stream -- and pulls bytes as it needs them, like the reference's source
+ * (source.go:99-122, io.ReadFull on the reader).  mp3.NewDecoder(r)
+ * (decode.go:361-388) is mp3g_decoder_new_reader: it returns once the tags
+ * and frame 0 are in (for a seeker, after the header walk of
+ * ensureFrameStartsAndLength, decode.go:154-216, as the reference does).
+ *   read : io.Reader.Read -- write up to `cap` bytes to `buf`, return the
+ *          count; 0 = io.EOF; < 0 = an error (the decoder call in progress
+ *          returns MP3G_ERR_READ; a later call asks the reader again).
+ *   seek : io.Seeker.Seek (whence 0/1/2), the new offset or < 0 on error; NULL
+ *          when the reader is no io.Seeker (Length = -1, Seek fails as the
+ *          reference's does, source.go:28-33).
+ *   user : passed back to the callbacks verbatim, never dereferenced (for
+ *          cgo: a runtime/cgo.Handle, not a Go pointer).
+ * Read-ahead policy: with a seek callback (a file-like source) the decoder
+ * reads ahead in batches; without one it calls `read` only when it holds no
+ * complete frame it has not decoded -- exactly when the reference's
+ * Decoder.Read blocks on its reader -- so every frame whose bytes have
+ * arrived is delivered without waiting for more input.  The callbacks run on
+ * the thread that calls into the decoder, only during that call. */
+typedef struct mp3g_reader {
+  int64_t (*read)(void* user, uint8_t* buf, size_t cap);
+  int64_t (*seek)(void* user, int64_t offset, int whence);
+  void* user;
+} mp3g_reader;
+int mp3g_decoder_new_reader(const mp3g_reader* reader, int device, uint32_t mode, mp3g_decoder** out);
 void mp3g_decoder_free(mp3g_decoder* dec);
 int mp3g_decoder_read(mp3g_decoder* dec, uint8_t* buf, size_t cap, size_t* n);
 /* io.ReadFull over Decoder.Read (Go's io.ReadFull loops Read the same way):

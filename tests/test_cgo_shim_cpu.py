@@ -16,7 +16,7 @@ HEADER = open(os.path.join(REPO, "include", "mp3g.h")).read()
 GO = {f: open(os.path.join(REPO, "go", f)).read() for f in sorted(os.listdir(os.path.join(REPO, "go")))
       if f.endswith(".go")}
 CGO_BUILTINS = {"malloc", "free", "CBytes", "GoString", "CString", "GoBytes"}
-C_SCALARS = {"int", "uint", "size_t", "int16_t", "uint8_t", "uint16_t", "uint32_t", "uint64_t", "int64_t",
+C_SCALARS = {"int", "uint", "size_t", "uintptr_t", "int16_t", "uint8_t", "uint16_t", "uint32_t", "uint64_t", "int64_t",
              "double", "float", "char"}
 
 
@@ -67,15 +67,33 @@ def test_go_shim_files_present():
         assert 'import "C"' in src and '#include "mp3g.h"' in src, f
 
 
+def preamble_functions(src):
+    """name -> parameter count of the C functions a Go file's cgo preamble
+    declares itself (helpers defined in the package's .c files)."""
+    pre = src.split('import "C"', 1)[0]
+    out = {}
+    for m in re.finditer(r"^\s*(?://\s*)?(?:int|void|int64_t)\s+\**(\w+)\(([^;{]*?)\);", pre, flags=re.M):
+        if m.group(0).lstrip().startswith("//"):
+            continue
+        params = m.group(2).strip()
+        out[m.group(1)] = 0 if params in ("", "void") else params.count(",") + 1
+    return out
+
+
 def test_c_identifiers_and_call_arity_match_the_header():
     protos = prototypes()
     hdr = _strip_comments(HEADER)
     for f, src in GO.items():
         code = _strip_comments(src.split('import "C"', 1)[1])
+        local = preamble_functions(src)
         for m in re.finditer(r"\bC\.(\w+)", code):
             name = m.group(1)
             after = code[m.end():m.end() + 1]
             if name in CGO_BUILTINS or name in C_SCALARS:
+                continue
+            if name in local:
+                got = call_args(code, m.end())
+                assert got == local[name], f"{f}: C.{name} called with {got} args, preamble declares {local[name]}"
                 continue
             if name.startswith("mp3g_") and after == "(" and name in protos:
                 got = call_args(code, m.end())
@@ -114,3 +132,28 @@ def test_struct_fields_written_by_the_shim_exist():
 def test_abi_version_matches():
     v = int(re.search(r"#define MP3G_ABI_VERSION (\d+)", HEADER).group(1))
     assert f"const ABIVersion = {v}" in GO["frame_mp3g.go"]
+
+
+def test_streaming_reader_trampolines():
+    """decoder_mp3g.go streams its io.Reader (ABI 3): the .c trampolines call
+    exactly the Go functions the Go file exports, with the mp3g_reader
+    callback signatures of the header, and hand the library the handle as the
+    user value; NewDecoder no longer reads the whole input first."""
+    csrc = open(os.path.join(REPO, "go", "reader_mp3g.c")).read()
+    go = GO["decoder_mp3g.go"]
+    assert csrc.startswith("//go:build mp3g")
+    exported = set(re.findall(r"^//export (\w+)", go, flags=re.M))
+    assert exported == {"mp3gGoRead", "mp3gGoSeek"}
+    for fn in exported:
+        assert re.search(r"\b%s\(\(uintptr_t\)user," % fn, csrc), fn
+    # the callback shapes of mp3g_reader
+    rd = re.search(r"typedef struct mp3g_reader \{(.*?)\} mp3g_reader;", _strip_comments(HEADER), flags=re.S).group(1)
+    assert "int64_t (*read)(void* user, uint8_t* buf, size_t cap);" in rd
+    assert "int64_t (*seek)(void* user, int64_t offset, int whence);" in rd
+    assert "static int64_t goreader_read(void* user, uint8_t* buf, size_t cap)" in csrc
+    assert "static int64_t goreader_seek(void* user, int64_t offset, int whence)" in csrc
+    assert "mp3g_decoder_new_reader(&r, device, mode, out)" in csrc
+    decl = re.search(r"int goreader_decoder_new\(([^)]*)\)", go).group(1)
+    assert decl == re.search(r"int goreader_decoder_new\(([^)]*)\)", csrc).group(1)
+    body = go[go.index("func NewDecoder("):go.index("func NewDecoderBytes(")]
+    assert "io.ReadAll" not in body and "cgo.NewHandle" in body

@@ -62,16 +62,26 @@ def _worker(rank, world, port, q):
         loc, lo, hi = mdist.shard_streams(s, world, rank)
         pcm, _ = oracle.dsp_streams(g[lo:hi], c[lo:hi], loc) if hi > lo else (np.zeros((0, 576, 2), np.int16), None)
         t = mdist.max_over_ranks(0.5 + rank)
-        out = mdist.gather_pcm(torch.from_numpy(np.ascontiguousarray(pcm).reshape(-1)))
+        mine = torch.from_numpy(np.ascontiguousarray(pcm).reshape(-1))
+        out = mdist.gather_pcm(mine)
+        # the same into one preallocated buffer on rank 0 (larger than needed:
+        # the tail stays untouched)
+        pre = torch.full((len(g) * 1152 + 99,), 7, dtype=torch.int16) if rank == 0 else None
+        out2 = mdist.gather_pcm(mine, out=pre)
         if rank == 0:
             want, _ = oracle.dsp_streams(g, c, s)
-            q.put(("ok", t, bool(np.array_equal(out.numpy().reshape(-1, 576, 2), want))))
+            same = np.array_equal(out.numpy().reshape(-1, 576, 2), want)
+            same2 = out2 is pre and np.array_equal(pre[:len(g) * 1152].numpy().reshape(-1, 576, 2), want) \
+                and bool((pre[len(g) * 1152:] == 7).all())
+            q.put(("ok", t, bool(same and same2)))
+        else:
+            assert out is None and out2 is None
         dist.barrier()
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 6])  # 6 ranks, 5 streams: one rank sends nothing
 def test_gloo_shard_and_gather(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

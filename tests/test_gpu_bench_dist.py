@@ -1,0 +1,48 @@
+"""bench.py's multi-rank branch, rehearsed on one GPU.
+
+The driver runs `bench.py --gpus N` under torch.distributed.run on a whole
+8-GPU node with RCCL; that branch (process group, barriers, max over ranks,
+the timed PCM gather to rank 0 into one preallocated buffer, the gathered
+PCM's parity) is exercised here as 2 ranks sharing cuda:0 over gloo, with
+the collectives staged through host memory.  torch.distributed.run starts
+the ranks as fresh processes; nothing in this test touches the GPU itself.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+@pytest.mark.parametrize("config", ["c2"])
+def test_bench_two_ranks_gloo(config):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--config", config, "--backend", "gloo", "--single-mode", "--no-bitstream", "--no-polyphase"]
+    env = dict(os.environ, OMP_NUM_THREADS="4")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=REPO, env=env)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert r.returncode == 0 and len(lines) == 1, r.stdout[-3000:] + r.stderr[-5000:]
+    d = json.loads(lines[0])
+    print({k: d[k] for k in ("value", "ms_per_step", "n_gpus", "gather_ms", "max_dpcm_lsb")})
+    assert d["n_gpus"] == 2 and d["steps"] == 2 and d["warmup"] == 1
+    assert d["value"] > 0 and d["ms_per_step"] > 0
+    assert d["scaling"] == "weak"
+    # the gather is timed apart from the decode and lands every rank's PCM
+    assert d["gather_ms"] > 0 and d["gather"]["bytes"] == 2 * 20000 * 2304
+    assert d["gather"]["parity"]["max_dpcm_lsb"] <= 1 and len(d["gather"]["parity"]["per_rank"]) == 2
+    # rank 0's own timed output against the oracle
+    assert d["max_dpcm_lsb"] <= 1 and d["modes"]["fast"]["parity_granules"] > 0
+    assert "cpu_baseline" not in d  # an N = 1 figure

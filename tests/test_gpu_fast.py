@@ -249,3 +249,47 @@ def test_fast_sparse_linbits_spikes(gpu):
     assert np.abs(lines).max() > 8.0
     pcm, _ = fast_plan(gpu, g, c, s)
     assert_close(pcm, want, "sparse linbits spikes")
+
+
+def _lsf_channel_switch_stream(pattern, n_frames, seed):
+    """An MPEG-2 LSF stream (one granule per frame) whose channel count follows
+    `pattern` (a string of 'M' / 'S' repeated over the frames)."""
+    mono_g, mono_c = synth.synth_stream(seed, n_frames, mode=synth.MODE_MONO, lsf=True, p_event=0.1)
+    st_g, st_c = synth.synth_stream(seed + 1, n_frames, mode=synth.MODE_JOINT, lsf=True, p_event=0.1, p_is=0.3)
+    sel = np.array([pattern[i % len(pattern)] == "S" for i in range(n_frames)])
+    g = np.where(sel, st_g, mono_g)
+    c = np.where(sel[:, None, None], st_c, mono_c)
+    return g, c, sel
+
+
+@pytest.mark.parametrize("pattern", ["MS", "SSM", "MMS", "SMM"])
+def test_fast_hot_zones_across_channel_switches(gpu, pattern):
+    """Hot granules right after mono <-> stereo switches of a one-granule-per-
+    frame (MPEG-2 LSF) stream: the hot-zone replay walks back over granules
+    whose channel count changes every frame, so whether a replayed granule's
+    channel-1 V is needed must come from its own header (it was
+    read from the descriptor the wave held last).  Reference order inside the
+    zones, +-1 LSB, chunking bit-identical, exported state within float noise."""
+    rng = np.random.default_rng(len(pattern) * 7 + pattern.count("S"))
+    n = 90
+    g, c, sel = _lsf_channel_switch_stream(pattern, n, seed=300 + len(pattern))
+    change = np.nonzero(sel[1:] != sel[:-1])[0] + 1
+    idx = np.unique(np.concatenate([change[::3], change[1::5] + 1, [n - 1]]))
+    idx = idx[idx < n]
+    for ch in range(2):
+        C = g["ch"][:, ch]
+        C["global_gain"][idx] = 230
+        C["count1"][idx] = 576
+    hot = rng.integers(-15, 16, size=(len(idx), 2, 576))
+    hot[~sel[idx], 1, :] = 0
+    c[idx] = hot
+    assert gpu.validate(g, c)[0] == 0
+    s = gpu.streams_for([n], gpu.STATE_OUT)
+    want, so_ref = oracle.dsp_streams(g, c, s)
+    serial, so_serial = fast_plan(gpu, g, c, s, chunk=n)
+    assert_close(serial, want, f"{pattern} serial")
+    for chunk in (1, 2, 3, 4, 7, 0):
+        pcm, so = fast_plan(gpu, g, c, s, chunk=chunk)
+        assert_close(pcm, want, f"{pattern} chunk={chunk}")
+        assert np.array_equal(pcm, serial), f"{pattern} chunk={chunk} differs from the serial run"
+        assert so.tobytes() == so_serial.tobytes(), f"{pattern} chunk={chunk}: exported state differs"

@@ -198,11 +198,19 @@ def test_c3_shape_bit_exact_and_batch_invariance(gpu):
     assert_pcm_equal(np.concatenate([p_a, p_b]), want, "c3 split batches")
 
 
-@pytest.mark.parametrize("variant", ["v1", "v2", "v4"])
+def test_v1_kernel_retired(gpu):
+    """The per-phase v1 exact kernel was retired in round 4 (ABI 3): asking for
+    it is an error, not a silent fallback to another kernel."""
+    with pytest.raises(gpu.Mp3gError) as e:
+        gpu.Plan(gpu.streams_for([4]), mode=gpu.FLAG_KERNEL_V1)
+    assert e.value.status == 8  # MP3G_ERR_UNSUPPORTED
+
+
+@pytest.mark.parametrize("variant", ["v2", "v4"])
 def test_kernel_variants_agree(gpu, captured, variant):
-    """Every exact kernel (per-phase v1, workgroup v2, one-wave v4 = the
-    default) is bit-exact on every case."""
-    mode = {"v1": gpu.FLAG_KERNEL_V1, "v2": gpu.FLAG_KERNEL_V2, "v4": 0}[variant]
+    """Every exact kernel (workgroup v2, one-wave v4 = the default) is
+    bit-exact on every case."""
+    mode = {"v2": gpu.FLAG_KERNEL_V2, "v4": 0}[variant]
     g, c, want = captured["classic_lame.mp3"]
     pcm, _ = run_plan(gpu, g, c, gpu.streams_for([len(g)]), chunk=7, mode=mode)
     assert_pcm_equal(pcm, want, variant)
