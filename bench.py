@@ -39,11 +39,15 @@ sys.path.insert(0, os.path.join(REPO, "go-mp3_amd"))
 BYTES_PER_GRANULE = 2 * 576 * 2 + 160 + 576 * 2 * 2
 BYTES_PER_FRAME = 2 * BYTES_PER_GRANULE  # MPEG-1 frame (2 granules)
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-# the DSP path is FP32-VALU-bound, report the flop roof beside
-# the HBM one: ~550 kflop per MPEG-1 stereo frame counted in the reference's
-# operation order (the fast kernel's transforms do fewer), against 157.3 TF/s
-# of FP32 with FMA; exact mode rounds every product and sum (no FMA): half that
-FLOPS_PER_FRAME = 550e3
+# SURVEY.md 8(d) asks for the flop roof beside the HBM one.  The flops are the
+# ones the kernel EXECUTES, from the f32 flop counters of the profile of the
+# same config (SQ_INSTS_VALU_FLOPS_FP32 + _TRANS, calibrated on known
+# instruction mixes: tools/flop_calib.hip, tools/summarize_profile.py),
+# against 157.3 TF/s of FP32 with FMA (exact mode never fuses, but its peak is
+# the same instruction rate; frac is executed flops / 157.3 TF).  The
+# reference's own operation count (~550 kflop per MPEG-1 stereo frame) is
+# reported beside it for scale only.
+REF_ORDER_FLOPS_PER_FRAME = 550e3
 FP32_PEAK_TFLOPS = 157.3
 METRIC = "MP3 frames/sec (44.1 kHz stereo 128 kbps) at 1/2/4/8 GPUs; max |ΔPCM| LSB"
 
@@ -386,6 +390,51 @@ def profiled_traffic(cfg, kernel):
     return None, None, None
 
 
+def profiled_duration(cfg, kernel):
+    """The kernel's average duration in the kept profile of the current set
+    (PMC-free kernel trace, launches of the timed size) and its path."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", f"{PROFILE_TAG}_{cfg}_*.json")), reverse=True):
+        d = json.load(open(f))
+        if kernel.split("::")[-1] in d.get("kernel", "") and d.get("avg_ns"):
+            return d["avg_ns"] / 1e6, os.path.relpath(f, REPO), d.get("duration_source")
+    return None, None, None
+
+
+def profile_check(cfg, kernel, alg_bytes):
+    ms, src, how = profiled_duration(cfg, kernel)
+    if ms is None:
+        return None
+    return {"kernel_ms": round(ms, 4), "frac": round(alg_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5),
+            "source": src, "duration_source": how}
+
+
+def profiled_flops(cfg, kernel):
+    """Executed f32 flops per launch of the kernel in the newest profile of the
+    current set for this config, and that profile's path, or (None, None)."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", f"{PROFILE_TAG}_{cfg}_*.json")), reverse=True):
+        d = json.load(open(f))
+        if kernel.split("::")[-1] in d.get("kernel", "") and d.get("executed_flops_per_launch"):
+            return d["executed_flops_per_launch"], os.path.relpath(f, REPO)
+    return None, None
+
+
+def flop_roofline(cfg, kernel, kern_ms, n_frames):
+    """SURVEY.md 8(d) flop roof on the kernel's executed flops (profile)."""
+    fl, src = profiled_flops(cfg, kernel)
+    out = {"peak_tflops": FP32_PEAK_TFLOPS, "flops_source": src,
+           "reference_order_flops_per_frame": REF_ORDER_FLOPS_PER_FRAME,
+           "reference_order_note": "the reference's operation count, for scale only (not executed, not in frac)"}
+    if fl is None:
+        out.update(achieved_tflops=None, frac=None)
+        return out
+    out.update(executed_flops_per_launch=fl, executed_flops_per_frame=round(fl / n_frames, 1),
+               achieved_tflops=round(fl / (kern_ms * 1e-3) / 1e12, 2),
+               frac=round(fl / (kern_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS, 4))
+    return out
+
+
 def host_info():
     """The box's CPU as the CPU baseline ran on it."""
     model = None
@@ -634,6 +683,9 @@ def main():
                          "traffic": traffic, "traffic_source": traffic_src,
                          "traffic_same_build": None if traffic_sha is None else traffic_sha == lib_sha16(),
                          "kernel": MODES[args.mode][1], "kernel_ms": round(kern_ms, 4),
+                         # the same roofline from the kept profile's kernel duration
+                         # (rocprofv3 kernel trace, no counters): reproducible from profiles/
+                         "profile": profile_check(args.config, MODES[args.mode][1], n_gran * BYTES_PER_GRANULE),
                          "algorithmic_bytes_per_frame": BYTES_PER_FRAME,
                          "algorithmic_bytes_per_launch": n_gran * BYTES_PER_GRANULE,
                          # what binds instead (DESIGN.md "Roofline"): VALU issue and
@@ -641,14 +693,9 @@ def main():
                          "issue": profiled_issue(args.config, MODES[args.mode][1])},
             "modes": {m: {"value": round(r["value"], 1), "kernel_ms": round(r["kernel_ms"], 4),
                           "kernel": MODES[m][1], "pcm": MODES[m][0],
-                          # SURVEY.md 8(d) flop roof (reference-order flops; exact: no-FMA ceiling)
-                          "flop_roofline": {
-                              "achieved_tflops": round(r["value"] / world * FLOPS_PER_FRAME / 1e12, 2),
-                              "peak_tflops": FP32_PEAK_TFLOPS if m == "fast" else FP32_PEAK_TFLOPS / 2,
-                              "frac": round(r["value"] / world * FLOPS_PER_FRAME / 1e12 /
-                                            (FP32_PEAK_TFLOPS if m == "fast" else FP32_PEAK_TFLOPS / 2), 4),
-                              "flops_per_frame": FLOPS_PER_FRAME} if args.config != "c5" else None}
-                      for m, r in res.items()},  # (c5: MPEG-2 mono frames, another flop count)
+                          # SURVEY.md 8(d) flop roof on EXECUTED flops (profile counters)
+                          "flop_roofline": flop_roofline(args.config, MODES[m][1], r["kernel_ms"], n_frames)}
+                      for m, r in res.items()},
         }
         if out["roofline"]["traffic_same_build"] is False:
             print("bench.py: warning: roofline traffic is from a profile of another build (%s)" % traffic_src,

@@ -945,15 +945,41 @@ __device__ __forceinline__ bool exact_granule(const mp3g_granule* __restrict__ g
   return hot;
 }
 
+// End (exclusive, clipped to the chunk) of the granules whose PCM reads a
+// hot granule g's V blocks.  Channel 0's V of g feeds the windows of g and
+// g + 1.  Channel 1's -- g stereo -- feeds g's window and that of the next
+// STEREO granule: a mono granule leaves channel 1's FIFO alone (Decode works
+// on ch < nch, frame.go:125-133), so across a mono run the zone reaches the
+// first stereo granule after it.  (Rare path: scalar header loads.)
+__device__ __forceinline__ uint32_t zone_end(const mp3g_granule* __restrict__ gran, uint32_t g, uint32_t end) {
+  uint32_t e = g + 2;
+  if (hdr_nch(__builtin_amdgcn_readfirstlane(gran[g].header)) == 2) {
+    uint32_t n = g + 1;
+    while (n < end && hdr_nch(__builtin_amdgcn_readfirstlane(gran[n].header)) == 1) n++;
+    if (n + 1 > e) e = n + 1;
+  }
+  return e < end ? e : end;
+}
+
 // Zones recorded by the fast pass (WaveSmem::zone): a hot granule g opens
 // (or extends) the zone [max(g, out_first), g + 2) of granules whose PCM
-// depends on its hybrid output (the window of g + 1 reads g's V blocks).
-// When the list is full the last zone runs to the chunk end.
+// depends on its hybrid output; the zone pass, which re-detects g as hot in
+// the reference's arithmetic, extends it to zone_end(g) (kept out of the
+// granule loop: its register budget).  (If the exact S of g is not hot, the
+// fast V of g is within the fast bound and nothing past g + 2 needs redoing.)
+// A replayed granule g < out_first whose V reaches an output only across a
+// mono run gets its zone_end here.  When the list is full the last zone runs
+// to the chunk end.
 template <class Smem>
-__device__ __forceinline__ void record_hot(Smem& s, uint32_t& nz, uint32_t g, uint32_t out_first, uint32_t end) {
+__device__ __forceinline__ void record_hot(Smem& s, uint32_t& nz, const mp3g_granule* __restrict__ gran, uint32_t g,
+                                           uint32_t out_first, uint32_t end) {
   // (wave-uniform throughout: every lane stores the same values)
-  const uint32_t zs = g > out_first ? g : out_first, ze = g + 2 < end ? g + 2 : end;
-  if (zs >= ze) return;  // a replayed granule whose V no output reads
+  const uint32_t zs = g > out_first ? g : out_first;
+  uint32_t ze = g + 2 < end ? g + 2 : end;
+  if (zs >= ze) {
+    ze = zone_end(gran, g, end);
+    if (zs >= ze) return;  // a replayed granule whose V no output reads
+  }
   const uint32_t last_end = nz ? __builtin_amdgcn_readfirstlane(s.zone[nz - 1][1]) : 0u;
   if (nz > 0 && zs <= last_end) {
     s.zone[nz - 1][1] = ze > last_end ? ze : last_end;
@@ -1532,7 +1558,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     // the second test (rare) on S in the ring: the granule's zone is redone
     // in the reference's order after the pass (a granule whose V feeds no
     // output needs no zone)
-    if (hot1 && need_v && slot_sums_hot(s.ring, nch)) record_hot(s, nz, g, out_first, end);
+    if (hot1 && need_v && slot_sums_hot(s.ring, nch)) record_hot(s, nz, gran, g, out_first, end);
 #endif
     stamp(4);
     {
@@ -1631,7 +1657,10 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       }
       for (; gz < ze; gz++) {
         const bool nv = replay_needs_v(gran, gz, zs);
-        if (exact_granule(gran, coef, pcm, s, sh, gz, gz >= zs, nv, zst)) ze = gz + 2 > ze ? (gz + 2 < end ? gz + 2 : end) : ze;
+        if (exact_granule(gran, coef, pcm, s, sh, gz, gz >= zs, nv, zst)) {
+          const uint32_t e = zone_end(gran, gz, end);
+          ze = e > ze ? e : ze;
+        }
       }
       done = gz;
     }

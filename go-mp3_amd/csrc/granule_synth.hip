@@ -283,7 +283,7 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
 #if MP3G_HOT_CHECK
     // a hot granule (two tests, the second rare and on the staged S): its
     // zone is redone in the reference's order after the pass
-    if (hot1 && slot_sums_hot<kSS>(s.ring, nch, cur)) record_hot(s, nz, g, out_first, end);
+    if (hot1 && slot_sums_hot<kSS>(s.ring, nch, cur)) record_hot(s, nz, gran, g, out_first, end);
 #endif
     // ---- matrixing (frame.go:642-648): lane (ch, slot) turns its S row into X ----
     {
@@ -381,7 +381,10 @@ granule_synth_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, co
         have = true;
       }
       for (; g < ze; g++)
-        if (synth_exact_granule(gran, lines, pcm, s, g, g >= zs)) ze = g + 2 > ze ? (g + 2 < end ? g + 2 : end) : ze;
+        if (synth_exact_granule(gran, lines, pcm, s, g, g >= zs)) {
+          const uint32_t e = zone_end(gran, g, end);
+          ze = e > ze ? e : ze;
+        }
       done = g;
     }
     if (done >= end) export_state(0);

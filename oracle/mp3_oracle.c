@@ -1146,7 +1146,7 @@ int orc_dsp_streams(const mp3g_granule* g, const int16_t* coef, const mp3g_strea
 void orc_hybrid_streams(const mp3g_granule* g, const int16_t* coef, const mp3g_stream* streams,
                         uint32_t n_streams, const mp3g_state* state_in, float* is_out) {
   ensure_init();
-  static float store[2][32][18];
+  static __thread float store[2][32][18]; /* per thread, as orc_synth_streams */
   for (uint32_t s = 0; s < n_streams; s++) {
     const mp3g_stream* S = &streams[s];
     if (S->flags & MP3G_STREAM_STATE_IN) memcpy(store, state_in[s].store, sizeof store);
@@ -1213,7 +1213,7 @@ int orc_synth_streams(const mp3g_granule* g, const float* is, const mp3g_stream*
                       uint32_t n_streams, const mp3g_state* state_in, mp3g_state* state_out,
                       int16_t* pcm) {
   ensure_init();
-  static mp3g_state st;
+  static __thread mp3g_state st; /* per thread: callers may run streams concurrently */
   for (uint32_t s = 0; s < n_streams; s++) {
     const mp3g_stream* S = &streams[s];
     if (S->flags & MP3G_STREAM_STATE_IN) st = state_in[s];

@@ -205,3 +205,30 @@ def test_synth_sparse_spikes(gpu):
     want, _ = oracle.synth_streams(g, lines, s)
     got, _ = run_synth(gpu, g, lines, s)
     assert_close(got, want, "sparse spikes")
+
+
+@pytest.mark.parametrize("pattern", ["MS", "SSM", "SMM", "SSMMM"])
+@pytest.mark.parametrize("kind", ["randsign", "gauss"])
+def test_synth_hot_across_channel_switches(gpu, pattern, kind):
+    """Hot granules in a one-granule-per-frame stream whose channel count
+    follows `pattern`: a hot stereo granule's channel-1 V blocks are read by
+    the next STEREO granule's window, across any mono run between (a mono
+    granule leaves channel 1 alone, frame.go:125-133), so its zone must reach
+    that granule.  +-1 LSB against the oracle, chunkings bit-identical."""
+    from test_gpu_fast import _lsf_channel_switch_stream
+    rng = np.random.default_rng(len(pattern) + 17 * len(kind))
+    n = 90
+    g, c, sel = _lsf_channel_switch_stream(pattern, n, seed=400 + len(pattern))
+    s = gpu.streams_for([n], gpu.STATE_OUT)
+    lines = oracle.hybrid_streams(g, c, s)
+    stereo_idx = np.nonzero(sel)[0]
+    idx = np.unique(np.concatenate([stereo_idx[::4], np.nonzero(~sel)[0][::7], [n - 1]]))
+    lines[idx] = hot_lines(rng, len(idx), kind, 1e4 if kind != "gauss" else 300.0)
+    lines[~sel, 1, :] = 0.0  # (a mono granule has no channel 1)
+    want, _ = oracle.synth_streams(g, lines, s)
+    serial, so_serial = run_synth(gpu, g, lines, s, chunk=n)
+    assert_close(serial, want, f"{pattern} {kind} serial")
+    for chunk in (1, 2, 3, 5, 0):
+        pcm, so = run_synth(gpu, g, lines, s, chunk=chunk)
+        assert np.array_equal(pcm, serial), f"{pattern} {kind} chunk={chunk} differs from the serial run"
+        assert so.tobytes() == so_serial.tobytes(), f"{pattern} {kind} chunk={chunk}: exported state differs"

@@ -1,9 +1,18 @@
 #!/usr/bin/env python3
-"""Summarize rocprofv3 passes (tools/profile.sh) into profiles/<tag>_<cfg>.json + copy stats CSVs.
+"""Summarize rocprofv3 passes (tools/profile.sh) into profiles/<tag>_<cfg>_<kernel>.json
+and copy the kernel-stats CSVs.
 
-HBM traffic per launch follows MI355X_MICROARCH.md (HBM section): FETCH_SIZE and
+  tools/summarize_profile.py <gpurun_out dir> <tag> <cfg> [algorithmic bytes per launch|-] [kernel substring]
+
+Kernel duration: the PMC-free `head` pass (the headline launches alone) when
+the kernel is in it, else the PMC-free `trace` pass; in both only the
+launches over the kernel's largest grid (the bench's timed size).  HBM
+traffic per launch follows MI355X_MICROARCH.md (HBM section): FETCH_SIZE and
 WRITE_SIZE come from separate --pmc passes, are in KiB, and FETCH_SIZE reads
 exactly half the bytes of a wide coalesced stream on gfx950 -> doubled.
+Executed flops: SQ_INSTS_VALU_FLOPS_FP32 (+ _TRANS) scaled by the calibration
+pass over tools/flop_calib (known instruction counts per kind), which also
+records how the counter weighs FMA and packed instructions.
 """
 import collections
 import csv
@@ -14,6 +23,9 @@ import shutil
 import sys
 
 KERNEL = "granule"
+CALIB = {  # tools/flop_calib kernels: f32 flops per lane-instruction by the usual convention
+    "calib_fma_f32": 2, "calib_add_f32": 1, "calib_mul_f32": 1, "calib_exp_f32": 1,
+    "calib_pk_fma_f32": 4, "calib_pk_mul_f32": 2, "calib_pk_add_f32": 2}
 
 
 def counters(d, kernel=None, grid=None):
@@ -29,9 +41,7 @@ def counters(d, kernel=None, grid=None):
 
 def full_launches(d, kernel):
     """(grid, durations in ns) of the kernel's launches over the largest grid
-    in the kernel trace: the bench's timed launches.  A bench run also makes
-    smaller launches of the same kernel (the pipelined bitstream API decodes
-    groups of streams), which the rocprof stats average in."""
+    in the kernel trace: the bench's timed launches."""
     f = glob.glob(os.path.join(d, "*kernel_trace.csv"))
     if not f:
         return None, []
@@ -43,25 +53,65 @@ def full_launches(d, kernel):
                   if int(r["Grid_Size_X"]) == grid]
 
 
+def calibration(src, tag, dst):
+    """Counter values per lane-instruction of each tools/flop_calib kernel."""
+    d = os.path.join(src, f"prof_{tag}_calib")
+    f = glob.glob(os.path.join(d, "*counter_collection.csv"))
+    if not f:
+        return None
+    out_f = glob.glob(os.path.join(src, f"prof_{tag}.log"))
+    lane_instr = None
+    for fn in out_f:
+        for line in open(fn):
+            if line.startswith("{\"lane_instructions\""):
+                lane_instr = json.loads(line)["lane_instructions"]
+    vals = collections.defaultdict(dict)
+    for r in csv.DictReader(open(f[0])):
+        name = r["Kernel_Name"].split("(")[0]
+        vals[name][r["Counter_Name"]] = vals[name].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    res = {"lane_instructions_per_kernel": lane_instr, "kernels": {}}
+    for k, want in CALIB.items():
+        v = vals.get(k)
+        if not v or not lane_instr:
+            continue
+        res["kernels"][k] = {c: x / lane_instr for c, x in sorted(v.items())}
+        res["kernels"][k]["expected_flops_per_lane_instr"] = want
+    # scale: executed flops = counter / (counter per expected flop), from the
+    # plain FMA kernel; the others show whether packed ops are weighed alike
+    fma = res["kernels"].get("calib_fma_f32", {})
+    if fma.get("SQ_INSTS_VALU_FLOPS_FP32"):
+        res["counter_per_flop"] = fma["SQ_INSTS_VALU_FLOPS_FP32"] / 2.0
+        res["consistency"] = {k: (v.get("SQ_INSTS_VALU_FLOPS_FP32", 0.0) + v.get("SQ_INSTS_VALU_FLOPS_FP32_TRANS", 0.0))
+                              / res["counter_per_flop"] / v["expected_flops_per_lane_instr"]
+                              for k, v in res["kernels"].items()}
+    os.makedirs(dst, exist_ok=True)
+    json.dump(res, open(os.path.join(dst, f"{tag}_flop_calib.json"), "w"), indent=1)
+    return res
+
+
 def main(src, tag, cfg, dst="profiles", bytes_per_launch=None, kernel=None, suffix=""):
     kernel = kernel or KERNEL
     base = os.path.join(src, f"prof_{tag}_{cfg}")
     stats = list(csv.DictReader(open(glob.glob(base + "_trace/*kernel_stats.csv")[0])))
     k = [r for r in stats if kernel in r["Name"]][0]
-    grid, durs = full_launches(base + "_trace", kernel)
+    grid, durs = full_launches(base + "_head", kernel)
+    dur_src = "head"
+    if not durs:
+        grid, durs = full_launches(base + "_trace", kernel)
+        dur_src = "trace"
     fetch = counters(base + "_fetch", kernel, grid).get("FETCH_SIZE")
     write = counters(base + "_write", kernel, grid).get("WRITE_SIZE")
     sq = counters(base + "_sq", kernel, grid)
+    fl = counters(base + "_flops", kernel, grid)
     out = {"tag": tag, "config": cfg, "kernel": k["Name"].split("(")[0],
            "stats_calls": int(k["Calls"]), "stats_avg_ns": float(k["AverageNs"])}
-    # the library build the passes ran (tools/profile.sh records its sha256):
-    # bench.py flags traffic read from a profile of another build
     shaf = os.path.join(src, f"prof_{tag}_lib.sha")
     if os.path.exists(shaf):
         out["lib_sha16"] = open(shaf).read().split()[0][:16]
-    if durs:  # the full-grid launches only (kernel trace)
+    if durs:
         avg_ns = sum(durs) / len(durs)
-        out.update(grid=grid, calls=len(durs), avg_ns=avg_ns, min_ns=min(durs), max_ns=max(durs))
+        out.update(grid=grid, calls=len(durs), avg_ns=avg_ns, min_ns=min(durs), max_ns=max(durs),
+                   duration_source=f"{dur_src} pass: rocprofv3 --kernel-trace, no counters, launches of grid {grid}")
     else:
         avg_ns = float(k["AverageNs"])
         out.update(calls=int(k["Calls"]), avg_ns=avg_ns, min_ns=float(k["MinNs"]), max_ns=float(k["MaxNs"]))
@@ -77,14 +127,22 @@ def main(src, tag, cfg, dst="profiles", bytes_per_launch=None, kernel=None, suff
             slots = 256 * 4 * (sq["GRBM_GUI_ACTIVE"] / 8) / 2
             if "SQ_INSTS_VALU" in sq:
                 out["valu_issue_util"] = sq["SQ_INSTS_VALU"] / slots
+    if fl:
+        out["flop_counters"] = fl
+        cal = calibration(src, tag, dst)
+        if cal and cal.get("counter_per_flop"):
+            f32 = (fl.get("SQ_INSTS_VALU_FLOPS_FP32", 0.0) + fl.get("SQ_INSTS_VALU_FLOPS_FP32_TRANS", 0.0))
+            out["executed_flops_per_launch"] = f32 / cal["counter_per_flop"]
+            out["executed_tflops"] = out["executed_flops_per_launch"] / avg_ns / 1e3
+            out["flop_calibration"] = f"profiles/{tag}_flop_calib.json"
     if bytes_per_launch:
         out["algorithmic_bytes_per_launch"] = bytes_per_launch
         out["algorithmic_gbps"] = bytes_per_launch / avg_ns
     os.makedirs(dst, exist_ok=True)
     json.dump(out, open(os.path.join(dst, f"{tag}_{cfg}{suffix}.json"), "w"), indent=1)
-    for kind in ("trace",):
+    for kind, name in (("trace", "kernel_stats"), ("head", "head_kernel_stats")):
         for f in glob.glob(base + f"_{kind}/*kernel_stats.csv"):
-            shutil.copyfile(f, os.path.join(dst, f"{tag}_{cfg}_kernel_stats.csv"))
+            shutil.copyfile(f, os.path.join(dst, f"{tag}_{cfg}_{name}.csv"))
     print(json.dumps(out, indent=1))
 
 
