@@ -417,18 +417,63 @@ MP3G_HD_INLINE int decode_job(const mp3g_hjob& job, uint64_t j, const uint64_t* 
         for (int sl = 0; sl < kBlk / 2; sl++) out.b[sl] = 0u;
       }
     }
+    // count1 quads (huffman.go:106-131), one writer block per step as well:
+    // every quad of the phase starts at a line = bv2 (mod 4), i.e. at dword
+    // slot 2q (even phase) or 2q + 1 (odd phase) of its 16-line block, so the
+    // four quad slots of a block write fixed registers (an odd phase's fourth
+    // quad carries its second dword into the next block).  The block holding
+    // bv2 starts with the pairs' partial block and skips the slots before it.
     i = bv2;
-    while (i <= 572 && r.pos <= pend) {
-      int a, b, c, d;
-      decode_sym<kSwap, true>(r, T, qroot, 0u, a, b, c, d);
-      out.put(i, a, b);
-      out.put(i + 2, c, d);
-      i += 4;
+    bool act = i <= 572 && r.pos <= pend;
+    const bool odd = (bv2 & 2) != 0;
+    const int k0 = (bv2 & (kBlk - 1)) >> 1;  // first free dword slot of the first block
+    bool pend_blk = act || k0 != 0;           // this block has lines to store
+    int blk = bv2 & ~(kBlk - 1);
+    bool first_blk = true;
+    uint32_t w[kBlk / 2];
+#pragma unroll
+    for (int sl = 0; sl < kBlk / 2; sl++) w[sl] = out.b[sl];
+    while (pend_blk) {
+      uint32_t carry = 0u;
+      bool carried = false;
+#pragma unroll
+      for (int q = 0; q < kBlk / 4; q++) {
+        const int slot = odd ? 2 * q + 1 : 2 * q;
+        if (act && (!first_blk || slot >= k0)) {
+          int a, b, c, d;
+          decode_sym<kSwap, true>(r, T, qroot, 0u, a, b, c, d);
+          const uint32_t v0 = (uint32_t)(uint16_t)(int16_t)a | ((uint32_t)(uint16_t)(int16_t)b << 16);
+          const uint32_t v1 = (uint32_t)(uint16_t)(int16_t)c | ((uint32_t)(uint16_t)(int16_t)d << 16);
+          if (odd) {
+            w[2 * q + 1] = v0;
+            if (q + 1 < kBlk / 4) {
+              w[2 * q + 2] = v1;
+            } else {
+              carry = v1;
+              carried = true;
+            }
+          } else {
+            w[2 * q] = v0;
+            w[2 * q + 1] = v1;
+          }
+          i += 4;
+          act = i <= 572 && r.pos <= pend;
+        }
+      }
+#pragma unroll
+      for (int sl = 0; sl < kBlk / 2; sl++) out.b[sl] = w[sl];
+      out.flush(blk);
+#pragma unroll
+      for (int sl = 0; sl < kBlk / 2; sl++) w[sl] = 0u;
+      w[0] = carry;
+      blk += kBlk;
+      first_blk = false;
+      pend_blk = act || carried;
     }
     count1 = i;
     if (r.pos > pend + 1) count1 = i >= 4 ? i - 4 : 0;  // the last word overran its part
   }
-  const int z = out.finish(i);
+  const int z = p23 ? (i + kBlk - 1) & ~(kBlk - 1) : out.finish(i);
   for (int k = count1; k < i; k++) row[k] = 0;  // lines the overrun check removed
   C.count1 = (uint16_t)count1;
   return z;
