@@ -144,6 +144,7 @@ def test_live_stream_new_decoder_returns_after_arrived_frames(gpu, sample_files,
     data = sample_files[name]
     cut = _frame_ends(data)[n_frames - 1]
     st_o, want = oracle.decode_all(data)
+    nb = n_frames * oracle.Decoder(data).bytes_per_frame  # 4,608 B per MPEG-1 frame, 2,304 per MPEG-2
     rfd, wfd = os.pipe()
     release = threading.Event()
 
@@ -160,7 +161,7 @@ def test_live_stream_new_decoder_returns_after_arrived_frames(gpu, sample_files,
             d = gpu.Decoder.from_reader(lambda n: os.read(rfd, n), None)
             got.put(("new", d.length))
             first = b""
-            while len(first) < n_frames * 4608:
+            while len(first) < nb:
                 st, b = d.read(4608)
                 if st != 0:
                     got.put(("status", st))
@@ -180,7 +181,7 @@ def test_live_stream_new_decoder_returns_after_arrived_frames(gpu, sample_files,
         assert (kind, length) == ("new", -1), (kind, length)
         kind, first = got.get(timeout=120)
         assert kind == "frames", (kind, first)
-        assert first == want[:n_frames * 4608]
+        assert first == want[:nb]
     finally:
         release.set()  # the rest of the stream arrives (also unblocks a failed run)
     kind, (st, rest) = got.get(timeout=120)
