@@ -143,17 +143,6 @@ struct __align__(16) WaveSmem {
   uint32_t zone[8][2];
 };
 constexpr uint32_t kZones = 8;
-// A chunk's hot zones, kept for the wave's zone pass after its chunk loop
-// (persistent kernel): the plan's launch scratch holds one per chunk, after
-// the two launch counters; `next` links the chunks of one wave with zones.
-struct ZoneRec {
-  uint32_t nz, next;
-  uint32_t zone[kZones][2];
-  uint32_t pad[2];
-};
-constexpr uint32_t kWorkWords = 8;  // launch counters (2 used), then ZoneRec[n_chunks]
-static_assert(sizeof(ZoneRec) == kZoneRecBytes && kWorkWords * 4 == sizeof(ChunkDesc), "launch scratch layout");
-constexpr uint32_t kNoChunk = 0xffffffffu;
 
 // Raw coefficients of lane (ch, sb) of granule g: its 18 lines, 36 B at
 // coef[g][ch][18 sb], as 9 dwords (two int16 each) by three 12-B buffer loads
@@ -1006,88 +995,6 @@ __device__ __forceinline__ void record_hot(Smem& s, uint32_t& nz, const mp3g_gra
 
 }  // namespace
 
-// Frame.store / vVec after the chunk's last granule (frame.go:48-49), from the
-// overlap pairs st (fast pass or zone replay) and the X history in the ring.
-__device__ __forceinline__ void export_state(const ChunkDesc& cd, mp3g_state* state_out, const WaveSmem& s,
-                                             const f2 (&st)[9]) {
-  if (!(cd.flags & kChunkStateOut)) return;
-  mp3g_state* so = state_out + cd.stream;
-  const int c = lane_fresh() >> 5, kk = lane_fresh() & 31;
-  const float sg = (kk & 1) ? -1.0f : 1.0f;
-#pragma unroll
-  for (int q = 0; q < 9; q++) {
-    so->store[c][kk][q] = (q & 1) ? st[q].x * sg : st[q].x;
-    so->store[c][kk][17 - q] = (q & 1) ? st[q].y : st[q].y * sg;
-  }
-  for (int e = lane_fresh(); e < 2 * 1024; e += kLanes) {
-    const int cc = e >> 10, blk = (e >> 6) & 15, i = e & 63;
-    so->vvec[cc][64 * blk + i] = blk < 15 ? v_from_x(&s.ring[cc][0][kHist - 1 - blk], i) : 0.0f;
-  }
-}
-
-// Hot zones of one chunk (rare): redo their granules in the reference's order
-// from their replay start (exact entry state) and overwrite their PCM; a zone
-// ends two granules after the last hot granule it meets.  Past a zone the fast
-// pass's own output stands: it depends on no hot granule's hybrid output.  A
-// zone reaching the chunk end also rewrites the exported state.  (The zones'
-// stages mirror the fast loop's, in the reference's operation order:
-// exact_granule.)  zone: the chunk's zone list (ZoneRec).
-__device__ __forceinline__ void replay_zones(const ChunkDesc& cd, uint32_t end, uint32_t nz, const uint32_t* zone,
-                                             const mp3g_granule* __restrict__ gran, const int16_t* __restrict__ coef,
-                                             int16_t* __restrict__ pcm, const mp3g_state* sin, mp3g_state* state_out,
-                                             WaveSmem& s, const SharedSmem& sh) {
-  f2 zst[9];          // the zones' own overlap state (nothing flows in from the fast pass)
-  uint32_t done = 0;  // the exact state in zst / the ring is valid for granules < done
-  bool have = false;
-  for (uint32_t i = 0; i < nz; i++) {
-    // (the wave wrote the record itself: coherent loads, past the L1)
-    const uint32_t zs = __builtin_amdgcn_readfirstlane(
-        __hip_atomic_load(&zone[2 * i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    uint32_t ze = __builtin_amdgcn_readfirstlane(
-        __hip_atomic_load(&zone[2 * i + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    if (have && ze <= done) continue;
-    uint32_t gz = done;
-    if (!have || zs > done) {  // a fresh zone: replay from its start's replay start
-      ChunkDesc cr = cd;
-      cr.out_first = zs;
-      cr.n_out = end - zs;
-      uint64_t wz;
-      int zin[2];
-      prologue(cr, gran, &wz, zin, lane_fresh());
-      init_state(s, sin, zin, lane_fresh(), zst);
-      gz = __builtin_amdgcn_readfirstlane((uint32_t)wz);
-      have = true;
-    }
-    for (; gz < ze; gz++) {
-      const bool nv = replay_needs_v(gran, gz, zs);
-      if (exact_granule(gran, coef, pcm, s, sh, gz, gz >= zs, nv, zst)) {
-        const uint32_t e = zone_end(gran, gz, end);
-        ze = e > ze ? e : ze;
-      }
-    }
-    done = gz;
-  }
-  if (done >= end) export_state(cd, state_out, s, zst);
-}
-
-// Chunk hand-out of the persistent one-wave kernels (fast v3; the launch holds
-// at most the resident workgroups): a wave's first chunk is its own index, the
-// next ones come from work[0], one atomic per chunk by lane 0.
-__device__ __forceinline__ uint32_t next_chunk(uint32_t* work, uint32_t n_waves, int lane) {
-  uint32_t v = 0u;
-  if (lane == 0) v = atomicAdd(&work[0], 1u);
-  return n_waves + __builtin_amdgcn_readfirstlane(v);
-}
-// A wave leaving the launch; the last one (every other wave has had its final
-// work[0] index returned) resets both counters for the plan's next launch,
-// which is ordered after this one on the plan's stream.
-__device__ __forceinline__ void leave(uint32_t* work, uint32_t n_waves, int lane) {
-  if (lane == 0 && atomicAdd(&work[1], 1u) == n_waves - 1u) {
-    __hip_atomic_store(&work[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&work[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
 // kStamp: diagnostic build -- per-phase s_memtime cycle sums of every wave go
 // to `stamps` (kPhases per workgroup); never used for output.
 constexpr int kPhases = 8;
@@ -1096,7 +1003,7 @@ __global__ void __launch_bounds__(kLanes * kWaves, MP3G_FAST_WAVES_PER_SIMD)
 granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, const mp3g_granule* __restrict__ gran,
                     const int16_t* __restrict__ coef, const mp3g_state* __restrict__ state_in,
                     mp3g_state* __restrict__ state_out, int16_t* __restrict__ pcm,
-                    unsigned long long* __restrict__ stamps, uint32_t* __restrict__ work) {
+                    unsigned long long* __restrict__ stamps) {
   unsigned long long ph[kPhases] = {}, tprev = 0, rt[4] = {};
   if constexpr (kStamp) rt[0] = __builtin_amdgcn_s_memrealtime();
   auto stamp = [&](int p) {
@@ -1108,7 +1015,8 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
   };
   __shared__ SharedSmem sh;
   __shared__ WaveSmem wsm[kWaves];
-  // the workgroup's tables, filled once (the waves then run chunk after chunk)
+  // the workgroup's tables, filled after each wave has issued its first
+  // loads: their latencies overlap
   auto shared_init = [&]() {
     const int t = threadIdx.x;
     for (int e = t; e < 4 * 2 * 9; e += kLanes * kWaves) {
@@ -1124,628 +1032,647 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     for (int e = t; e < kCombos * 32; e += kLanes * kWaves) (&sh.lband[0][0])[e] = (&g_fast.lband[0][0])[e];
   };
   const int lane = threadIdx.x & (kLanes - 1);
-  // Persistent waves: the launch holds at most the resident workgroups, and a
-  // wave takes chunks one after another -- its first by its index, the next
-  // ones from a launch-wide counter (work[0]) -- instead of retiring with its
-  // chunk.  A workgroup's LDS is only freed when its last wave ends, so with
-  // one chunk per wave the finished waves of a workgroup held their slots
-  // until its slowest chunk was done.  The last wave to leave resets the
-  // counters (work[1] counts the waves out) for the plan's next launch.
-  const uint32_t n_waves = gridDim.x * kWaves;
   // wave-uniform in an SGPR: the chunk descriptor then comes in by scalar
   // loads and its fields (pointers, counts) stay out of the VGPR budget
-  uint32_t ci = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + (threadIdx.x >> 6));
+  const uint32_t ci = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + (threadIdx.x >> 6));
+  if (ci >= n_chunks) {  // (wave-uniform: one barrier per wave either way)
+    shared_init();
+    __syncthreads();
+    return;
+  }
   WaveSmem& s = wsm[threadIdx.x >> 6];
+  const ChunkDesc cd = chunks[ci];
   const int ch = lane >> 5, k = lane & 31;
   // ring positions of the two X values the window of output i = k reads
   const int pa = dct32::kPosOfM[k < 16 ? 16 + k : (k == 16 ? 0 : 48 - k)];
   const int pb = dct32::kPosOfM[k < 16 ? 16 - k : k - 16];
-  uint32_t zhead = kNoChunk;  // the last chunk of this wave with hot zones
+
+  uint64_t w64;
+  int init_in[2];
+  prologue(cd, gran, &w64, init_in, lane);
+  // loop state as wave-uniform 32-bit scalars (plans are limited to < 2^32
+  // granules): keeps it in SGPRs, so per-granule header reads are scalar loads
+  // (lgkmcnt) that never wait behind the prefetch loads or PCM stores (vmcnt)
+  const uint32_t w = __builtin_amdgcn_readfirstlane((uint32_t)w64);
+  const uint32_t out_first = __builtin_amdgcn_readfirstlane((uint32_t)cd.out_first);
+  const uint32_t end = __builtin_amdgcn_readfirstlane((uint32_t)(cd.out_first + cd.n_out));
+  const mp3g_state* sin = state_in ? state_in + cd.stream : nullptr;
+
+
+  // entry state: overlap store in registers, V history as X vectors
+  // IMDCT overlap `store` (frame.go:473-476) in registers as pairs
+  // stp[q] = (store[q], store[17-q]), each element times the frequency-inversion
+  // sign of its line (odd line of an odd subband: -1), so the overlap-add
+  // yields frequency-inverted output directly
+  const float sodd = (k & 1) ? -1.0f : 1.0f;  // sign of the odd lines of this subband
+  f2 stp[9];
+  {
+    // (no dynamic indexing of init_in[]: a private array would be promoted to LDS)
+    const bool in0 = init_in[0] && sin, in1 = init_in[1] && sin;
+    const bool from_in = ch ? in1 : in0;
+#pragma unroll
+    for (int q = 0; q < 9; q++) {
+      const float a = from_in ? sin->store[ch][k][q] : 0.0f, b = from_in ? sin->store[ch][k][17 - q] : 0.0f;
+      stp[q] = (f2){(q & 1) ? a * sodd : a, (q & 1) ? b : b * sodd};
+    }
+    for (int e = lane; e < 2 * 15 * 32; e += kLanes) {
+      const int c = e / (15 * 32), blk = (e >> 5) % 15, m = e & 31;
+      const bool in = c ? in1 : in0;
+      s.ring[c][dct32::kPosOfM[m]][kHist - 1 - blk] = in ? x_from_v(&sin->vvec[c][64 * blk], m) : 0.0f;
+    }
+  }
+
+  uint32_t cw[9] = {};  // the current granule's raw coefficients (lane's 18 lines)
+  if (w < end) {
+    load_lines_lim(coef, w, lane, cw, (int)(MP3G_COEF_PER_GRANULE * sizeof(int16_t)), count1_lim(gran, w, lane));
+    if (lane < 10) reinterpret_cast<uint4*>(&s.desc)[lane] = reinterpret_cast<const uint4*>(gran + w)[lane];
+    if (lane < 10 && w + 1 < end)
+      reinterpret_cast<uint4*>(&s.descn)[lane] = reinterpret_cast<const uint4*>(gran + w + 1)[lane];
+  }
   shared_init();
   __syncthreads();  // the only workgroup barrier: the waves are independent from here on
-  for (; ci < n_chunks; ci = next_chunk(work, n_waves, lane)) {
-    if constexpr (kStamp) {
-      for (int p = 0; p < kPhases; p++) ph[p] = 0;
-      rt[0] = __builtin_amdgcn_s_memrealtime();
+
+  // PCM of a granule: one dword (L, R) per lane and slot pair
+  uint32_t pk[9] = {};
+  const int hi = lane >> 5;
+
+  // ---- 16-tap window over the X ring -> s16 PCM, stored straight to HBM ----
+  // (lanes of an absent channel compute values that are never stored; the
+  // PCM stores are issued for replayed granules too, through a resource with
+  // no records)
+  auto window_store = [&](uint32_t g, bool out, int nch) {
+    if (out) {
+      float dw[16];
+      {
+        const float4* d4 = reinterpret_cast<const float4*>(&sh.dwin[k][0]);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const float4 v = d4[q];
+          dw[4 * q] = v.x;
+          dw[4 * q + 1] = v.y;
+          dw[4 * q + 2] = v.z;
+          dw[4 * q + 3] = v.w;
+        }
+      }
+      // accumulator pair p = output slots (2p, 2p+1).  Tap 2t of the pair reads
+      // column a of rows (v, v+1) and tap 2t+1 column b of rows (v-1, v),
+      // v = 2p - 2t: every operand pair is two rows of one column, i.e. one
+      // ds_read2_b32 that lands as the packed operand, and each feeds up to 8
+      // accumulator pairs.
+      const f2* RA = reinterpret_cast<const f2*>(&s.ring[ch][pa][0]);
+      const float* RB = &s.ring[ch][pb][0];
+      f2 acc2[9];
+#pragma unroll
+      for (int p = 0; p < 9; p++) acc2[p] = bcast(0.0f);
+#pragma unroll
+      for (int v = -14; v <= 16; v += 2) {
+        const f2 A = RA[(kHist + v) / 2];  // slots (16+v, 17+v): 8-B aligned
+        const f2 B = {RB[kHist + v - 1], RB[kHist + v]};
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+          const int p = v / 2 + t;
+          if (p >= 0 && p < 9) {
+            acc2[p] = pfma(bcast(dw[2 * t]), A, acc2[p]);
+            acc2[p] = pfma(bcast(dw[2 * t + 1]), B, acc2[p]);
+          }
+        }
+      }
+      // (L, R) sample pairs without LDS staging: one v_permlane32_swap per slot
+      // pair hands lane i slot 2p's (L, R) and lane 32 + i slot 2p + 1's, so
+      // every lane stores one dword per slot pair and the wave 2 x 128
+      // contiguous bytes.  Mono: the swap hands lane i channel 0's slot 2p and
+      // lane 32 + i its slot 2p + 1, stored in both halves (frame.go:671-678).
+      auto pack = [&](auto mono) {
+#pragma unroll
+        for (int p = 0; p < 9; p++) {
+          const int a = (int)__builtin_amdgcn_fmed3f(acc2[p].x, -32767.0f, 32767.0f);
+          const int b = (int)__builtin_amdgcn_fmed3f(acc2[p].y, -32767.0f, 32767.0f);
+          const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+          // low halves of (r[0], r[1]) -> one dword: L | R << 16 (R = L for mono)
+          pk[p] = __builtin_amdgcn_perm((uint32_t)(decltype(mono)::value ? r[0] : r[1]), (uint32_t)r[0], 0x05040100u);
+        }
+      };
+      if (nch == 2) pack(std::false_type{});
+      else pack(std::true_type{});
+      // stored right away: a store's data registers are free again once it
+      // has issued (no s_waitcnt before their reuse on gfx950), and the loads
+      // this wave waits for next were issued before these stores
     }
-    const ChunkDesc cd = chunks[ci];
-
-    uint64_t w64;
-    int init_in[2];
-    prologue(cd, gran, &w64, init_in, lane);
-    // loop state as wave-uniform 32-bit scalars (plans are limited to < 2^32
-    // granules): keeps it in SGPRs, so per-granule header reads are scalar loads
-    // (lgkmcnt) that never wait behind the prefetch loads or PCM stores (vmcnt)
-    const uint32_t w = __builtin_amdgcn_readfirstlane((uint32_t)w64);
-    const uint32_t out_first = __builtin_amdgcn_readfirstlane((uint32_t)cd.out_first);
-    const uint32_t end = __builtin_amdgcn_readfirstlane((uint32_t)(cd.out_first + cd.n_out));
-    const mp3g_state* sin = state_in ? state_in + cd.stream : nullptr;
-
-
-    // entry state: overlap store in registers, V history as X vectors
-    // IMDCT overlap `store` (frame.go:473-476) in registers as pairs
-    // stp[q] = (store[q], store[17-q]), each element times the frequency-inversion
-    // sign of its line (odd line of an odd subband: -1), so the overlap-add
-    // yields frequency-inverted output directly
-    const float sodd = (k & 1) ? -1.0f : 1.0f;  // sign of the odd lines of this subband
-    f2 stp[9];
     {
-      // (no dynamic indexing of init_in[]: a private array would be promoted to LDS)
-      const bool in0 = init_in[0] && sin, in1 = init_in[1] && sin;
-      const bool from_in = ch ? in1 : in0;
+      const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
+          pcm + (size_t)g * 1152, (short)0, out ? MP3G_PCM_BYTES_PER_GRANULE : 0, 0x00020000);
+#pragma unroll
+      for (int p = 0; p < 9; p++)
+        __builtin_amdgcn_raw_buffer_store_b32(pk[p], rp, 4 * (32 * (2 * p + hi) + k), 0, 2);  // non-temporal: c2 -1.9 %, c3 -0.8 %
+    }
+  };
+
+  if constexpr (kStamp) {
+    tprev = __builtin_amdgcn_s_memtime();
+    rt[1] = __builtin_amdgcn_s_memrealtime();
+  }
+  // Progress-balanced issue priority.  The SIMD arbitrates VALU issue by
+  // priority, then age (MI355X_MICROARCH.md, two waves per SIMD), so at equal
+  // priority the oldest of the ~3 waves sharing a SIMD runs ahead and the
+  // youngest finishes last, alone and latency-bound (c2 timeline: loop spans
+  // 34 .. 101 us for identical chunks).  A wave with more of its chunk left
+  // takes a higher priority, which keeps the co-resident waves abreast.
+  const uint32_t span = end - w, span2 = 2 * span, span3 = 3 * span;
+  uint32_t nz = 0;  // hot zones recorded (s.zone)
+  for (uint32_t g = w; g < end; g++) {
+    if (MP3G_FAST_PRIO) {
+      const uint32_t left4 = 4u * (end - g);  // priority floor(4 * left / span), 3 .. 0
+      if (left4 > span3) __builtin_amdgcn_s_setprio(3);
+      else if (left4 > span2) __builtin_amdgcn_s_setprio(2);
+      else if (left4 > span) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+    }
+    const bool out = g >= out_first;
+    // does a replayed granule's V feed anything? (see v2 / DESIGN.md halo)
+    bool need_v = true;
+    if (!out && g + 1 < out_first) need_v = hdr_nch(gran[g + 1].header) < hdr_nch(s.desc.header);
+    // wave-uniform (SGPR): the per-combo tables below become scalar loads
+    const uint32_t h = __builtin_amdgcn_readfirstlane(s.desc.header);
+    const int nch = hdr_nch(h), combo = hdr_combo(h);
+    const bool act = ch < nch;
+    // the channels' scalar parameters in SGPRs (one 8-B LDS read each):
+    // dword 0 = count1 | global_gain << 16 | scalefac_scale << 24,
+    // dword 1 = preflag | win_switch_flag << 8 | block_type << 16 | mixed_block_flag << 24
+    uint32_t cp0[2], cp1[2];
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+      const uint2 v = *reinterpret_cast<const uint2*>(&s.desc.ch[c]);
+      cp0[c] = __builtin_amdgcn_readfirstlane(v.x);
+      cp1[c] = __builtin_amdgcn_readfirstlane(v.y);
+    }
+    auto is_short = [](uint32_t d1) { return (d1 & 0x00ffff00u) == 0x00020100u; };  // win_switch 1, block_type 2
+    // wave-uniform: every channel of this granule is a long block (no reorder)
+    const bool all_long = !is_short(cp1[0]) && (nch == 1 || !is_short(cp1[1]));
+    // this lane's channel (lanes of an absent channel mirror channel 0's block
+    // layout: no extra divergence)
+    const uint32_t d0 = (act && ch) ? cp0[1] : cp0[0], d1 = (act && ch) ? cp1[1] : cp1[0];
+
+    // ---- per-granule front-end parameters: band exponents (long bands only
+    //      when no channel has short blocks) ----
+    {
+      // long bands: lane = (c, sfb), 44 lanes
+      const int e = lane_fresh();
+      if (e < 44) {
+        const int c = e >= 22, sfb = e - 22 * c;
+        const uint32_t a0 = c ? cp0[1] : cp0[0], a1 = c ? cp1[1] : cp1[0];
+        const int v = (int)((a0 >> 16) & 0xffu) - 210 -
+                      ((a0 >> 24) ? 4 : 2) * ((int)s.desc.ch[c].scalefac_l[sfb] + (int)(a1 & 0xffu) * kPretab(sfb));
+        s.expo[e] = (_Float16)(0.25f * (float)v);
+      }
+      if (!all_long) {
+        // short bands: (c, sfb, win), 78 entries
+        for (int r0 = e; r0 < 2 * 39; r0 += kLanes) {
+          const int c = r0 >= 39, r = r0 - 39 * c, sfb = r / 3, win = r - 3 * sfb;
+          const uint32_t a0 = c ? cp0[1] : cp0[0];
+          const mp3g_channel& D = s.desc.ch[c];
+          const int v = (int)((a0 >> 16) & 0xffu) - 210 - 8 * (int)D.subblock_gain[win] -
+                        ((a0 >> 24) ? 4 : 2) * (int)D.scalefac_s[sfb][win];
+          s.expo[44 + r0] = (_Float16)(0.25f * (float)v);
+        }
+      }
+    }
+    const int count1 = (int)(d0 & 0xffffu);
+    const bool shortblk = is_short(d1);
+    const bool mixed = (d1 >> 24) != 0;
+    wave_sync();
+    stamp(0);
+
+    // ---- front end: requantize (gather through the reorder), lane = (ch, sb = k) ----
+    // the lane's 18 line-info words and raw integers are loaded in bulk first
+    float x[18];
+    if (all_long) {
+      int xi[18];
 #pragma unroll
       for (int q = 0; q < 9; q++) {
-        const float a = from_in ? sin->store[ch][k][q] : 0.0f, b = from_in ? sin->store[ch][k][17 - q] : 0.0f;
-        stp[q] = (f2){(q & 1) ? a * sodd : a, (q & 1) ? b : b * sodd};
+        xi[2 * q] = (int)(int16_t)(cw[q] & 0xffffu);
+        xi[2 * q + 1] = (int)(int16_t)(cw[q] >> 16);
       }
-      for (int e = lane; e < 2 * 15 * 32; e += kLanes) {
-        const int c = e / (15 * 32), blk = (e >> 5) % 15, m = e & 31;
-        const bool in = c ? in1 : in0;
-        s.ring[c][dct32::kPosOfM[m]][kHist - 1 - blk] = in ? x_from_v(&sin->vvec[c][64 * blk], m) : 0.0f;
-      }
-    }
-
-    uint32_t cw[9] = {};  // the current granule's raw coefficients (lane's 18 lines)
-    if (w < end) {
-      load_lines_lim(coef, w, lane, cw, (int)(MP3G_COEF_PER_GRANULE * sizeof(int16_t)), count1_lim(gran, w, lane));
-      if (lane < 10) reinterpret_cast<uint4*>(&s.desc)[lane] = reinterpret_cast<const uint4*>(gran + w)[lane];
-      if (lane < 10 && w + 1 < end)
-        reinterpret_cast<uint4*>(&s.descn)[lane] = reinterpret_cast<const uint4*>(gran + w + 1)[lane];
-    }
-
-    // PCM of a granule: one dword (L, R) per lane and slot pair
-    uint32_t pk[9] = {};
-    const int hi = lane >> 5;
-
-    // ---- 16-tap window over the X ring -> s16 PCM, stored straight to HBM ----
-    // (lanes of an absent channel compute values that are never stored; the
-    // PCM stores are issued for replayed granules too, through a resource with
-    // no records)
-    auto window_store = [&](uint32_t g, bool out, int nch) {
-      if (out) {
-        float dw[16];
-        {
-          const float4* d4 = reinterpret_cast<const float4*>(&sh.dwin[k][0]);
+      // long band of line j: first band of the subband + band starts among
+      // lines 1..j.  Every long band starts at an even line (consts.go:68-97
+      // SfBandIndices; dsp_tables.cpp checks it), so lines 2q and 2q + 1
+      // share one band: one exponent read per line pair.
+      const uint32_t lb = sh.lband[combo][lane_fresh() & 31];  // (lane recomputed: no spilled address)
+      _Float16 ex[9];
 #pragma unroll
-          for (int q = 0; q < 4; q++) {
-            const float4 v = d4[q];
-            dw[4 * q] = v.x;
-            dw[4 * q + 1] = v.y;
-            dw[4 * q + 2] = v.z;
-            dw[4 * q + 3] = v.w;
-          }
-        }
-        // accumulator pair p = output slots (2p, 2p+1).  Tap 2t of the pair reads
-        // column a of rows (v, v+1) and tap 2t+1 column b of rows (v-1, v),
-        // v = 2p - 2t: every operand pair is two rows of one column, i.e. one
-        // ds_read2_b32 that lands as the packed operand, and each feeds up to 8
-        // accumulator pairs.
-        const f2* RA = reinterpret_cast<const f2*>(&s.ring[ch][pa][0]);
-        const float* RB = &s.ring[ch][pb][0];
-        f2 acc2[9];
+      for (int q = 0; q < 9; q++)
+        ex[q] = s.expo[22 * ch + (int)(lb & 31u) + __builtin_popcount((lb >> 5) & ((2u << (2 * q)) - 1u))];
+      // Lines >= count1 hold zeros (the bitstream parse's guarantee,
+      // maindata/huffman.go:130-134; mp3g_validate checks it), and requantizing
+      // 0 gives 0, so long blocks need no per-line count1 test here.
+      // (absent-channel lanes compute garbage that nothing reads)
 #pragma unroll
-        for (int p = 0; p < 9; p++) acc2[p] = bcast(0.0f);
+      for (int j = 0; j < 18; j++) x[j] = requant_fast(xi[j], ex[j >> 1]);
+    } else {
+      int nsfs = 0;  // short bands whose first line lies below count1 (frame.go:229-255 loop bound)
 #pragma unroll
-        for (int v = -14; v <= 16; v += 2) {
-          const f2 A = RA[(kHist + v) / 2];  // slots (16+v, 17+v): 8-B aligned
-          const f2 B = {RB[kHist + v - 1], RB[kHist + v]};
-#pragma unroll
-          for (int t = 0; t < 8; t++) {
-            const int p = v / 2 + t;
-            if (p >= 0 && p < 9) {
-              acc2[p] = pfma(bcast(dw[2 * t]), A, acc2[p]);
-              acc2[p] = pfma(bcast(dw[2 * t + 1]), B, acc2[p]);
-            }
-          }
-        }
-        // (L, R) sample pairs without LDS staging: one v_permlane32_swap per slot
-        // pair hands lane i slot 2p's (L, R) and lane 32 + i slot 2p + 1's, so
-        // every lane stores one dword per slot pair and the wave 2 x 128
-        // contiguous bytes.  Mono: the swap hands lane i channel 0's slot 2p and
-        // lane 32 + i its slot 2p + 1, stored in both halves (frame.go:671-678).
-        auto pack = [&](auto mono) {
-#pragma unroll
-          for (int p = 0; p < 9; p++) {
-            const int a = (int)__builtin_amdgcn_fmed3f(acc2[p].x, -32767.0f, 32767.0f);
-            const int b = (int)__builtin_amdgcn_fmed3f(acc2[p].y, -32767.0f, 32767.0f);
-            const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
-            // low halves of (r[0], r[1]) -> one dword: L | R << 16 (R = L for mono)
-            pk[p] = __builtin_amdgcn_perm((uint32_t)(decltype(mono)::value ? r[0] : r[1]), (uint32_t)r[0], 0x05040100u);
-          }
-        };
-        if (nch == 2) pack(std::false_type{});
-        else pack(std::true_type{});
-        // stored right away: a store's data registers are free again once it
-        // has issued (no s_waitcnt before their reuse on gfx950), and the loads
-        // this wave waits for next were issued before these stores
-      }
+      for (int b = 0; b < 13; b++) nsfs += 3 * (int)g_fast.sfb_short[combo][b] < count1;
+      // reorder gather: the channel's raw lines staged in the current slots of
+      // the ring, lane (ch, sb) writing its 9 dwords to column sb
       {
-        const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
-            pcm + (size_t)g * 1152, (short)0, out ? MP3G_PCM_BYTES_PER_GRANULE : 0, 0x00020000);
+        uint32_t* col = reinterpret_cast<uint32_t*>(&s.ring[ch][k][kHist]);
 #pragma unroll
-        for (int p = 0; p < 9; p++)
-          __builtin_amdgcn_raw_buffer_store_b32(pk[p], rp, 4 * (32 * (2 * p + hi) + k), 0, 2);  // non-temporal: c2 -1.9 %, c3 -0.8 %
+        for (int q = 0; q < 9; q++) col[q] = cw[q];
       }
-    };
-
-    if constexpr (kStamp) {
-      tprev = __builtin_amdgcn_s_memtime();
-      rt[1] = __builtin_amdgcn_s_memrealtime();
-    }
-    // Progress-balanced issue priority.  The SIMD arbitrates VALU issue by
-    // priority, then age (MI355X_MICROARCH.md, two waves per SIMD), so at equal
-    // priority the oldest of the ~3 waves sharing a SIMD runs ahead and the
-    // youngest finishes last, alone and latency-bound (c2 timeline: loop spans
-    // 34 .. 101 us for identical chunks).  A wave with more of its chunk left
-    // takes a higher priority, which keeps the co-resident waves abreast.
-    const uint32_t span = end - w, span2 = 2 * span, span3 = 3 * span;
-    uint32_t nz = 0;  // hot zones recorded (s.zone)
-    for (uint32_t g = w; g < end; g++) {
-      if (MP3G_FAST_PRIO) {
-        const uint32_t left4 = 4u * (end - g);  // priority floor(4 * left / span), 3 .. 0
-        if (left4 > span3) __builtin_amdgcn_s_setprio(3);
-        else if (left4 > span2) __builtin_amdgcn_s_setprio(2);
-        else if (left4 > span) __builtin_amdgcn_s_setprio(1);
-        else __builtin_amdgcn_s_setprio(0);
-      }
-      const bool out = g >= out_first;
-      // does a replayed granule's V feed anything? (see v2 / DESIGN.md halo)
-      bool need_v = true;
-      if (!out && g + 1 < out_first) need_v = hdr_nch(gran[g + 1].header) < hdr_nch(s.desc.header);
-      // wave-uniform (SGPR): the per-combo tables below become scalar loads
-      const uint32_t h = __builtin_amdgcn_readfirstlane(s.desc.header);
-      const int nch = hdr_nch(h), combo = hdr_combo(h);
-      const bool act = ch < nch;
-      // the channels' scalar parameters in SGPRs (one 8-B LDS read each):
-      // dword 0 = count1 | global_gain << 16 | scalefac_scale << 24,
-      // dword 1 = preflag | win_switch_flag << 8 | block_type << 16 | mixed_block_flag << 24
-      uint32_t cp0[2], cp1[2];
-#pragma unroll
-      for (int c = 0; c < 2; c++) {
-        const uint2 v = *reinterpret_cast<const uint2*>(&s.desc.ch[c]);
-        cp0[c] = __builtin_amdgcn_readfirstlane(v.x);
-        cp1[c] = __builtin_amdgcn_readfirstlane(v.y);
-      }
-      auto is_short = [](uint32_t d1) { return (d1 & 0x00ffff00u) == 0x00020100u; };  // win_switch 1, block_type 2
-      // wave-uniform: every channel of this granule is a long block (no reorder)
-      const bool all_long = !is_short(cp1[0]) && (nch == 1 || !is_short(cp1[1]));
-      // this lane's channel (lanes of an absent channel mirror channel 0's block
-      // layout: no extra divergence)
-      const uint32_t d0 = (act && ch) ? cp0[1] : cp0[0], d1 = (act && ch) ? cp1[1] : cp1[0];
-
-      // ---- per-granule front-end parameters: band exponents (long bands only
-      //      when no channel has short blocks) ----
-      {
-        // long bands: lane = (c, sfb), 44 lanes
-        const int e = lane_fresh();
-        if (e < 44) {
-          const int c = e >= 22, sfb = e - 22 * c;
-          const uint32_t a0 = c ? cp0[1] : cp0[0], a1 = c ? cp1[1] : cp1[0];
-          const int v = (int)((a0 >> 16) & 0xffu) - 210 -
-                        ((a0 >> 24) ? 4 : 2) * ((int)s.desc.ch[c].scalefac_l[sfb] + (int)(a1 & 0xffu) * kPretab(sfb));
-          s.expo[e] = (_Float16)(0.25f * (float)v);
-        }
-        if (!all_long) {
-          // short bands: (c, sfb, win), 78 entries
-          for (int r0 = e; r0 < 2 * 39; r0 += kLanes) {
-            const int c = r0 >= 39, r = r0 - 39 * c, sfb = r / 3, win = r - 3 * sfb;
-            const uint32_t a0 = c ? cp0[1] : cp0[0];
-            const mp3g_channel& D = s.desc.ch[c];
-            const int v = (int)((a0 >> 16) & 0xffu) - 210 - 8 * (int)D.subblock_gain[win] -
-                          ((a0 >> 24) ? 4 : 2) * (int)D.scalefac_s[sfb][win];
-            s.expo[44 + r0] = (_Float16)(0.25f * (float)v);
-          }
-        }
-      }
-      const int count1 = (int)(d0 & 0xffffu);
-      const bool shortblk = is_short(d1);
-      const bool mixed = (d1 >> 24) != 0;
       wave_sync();
-      stamp(0);
-
-      // ---- front end: requantize (gather through the reorder), lane = (ch, sb = k) ----
-      // the lane's 18 line-info words and raw integers are loaded in bulk first
-      float x[18];
-      if (all_long) {
-        int xi[18];
+      const int16_t* rch = reinterpret_cast<const int16_t*>(&s.ring[ch][0][kHist]);
+      // line info through a buffer resource (SGPR base, 32-bit lane offset) and
+      // the lane's first line recomputed here: nothing of this rare path stays
+      // live (in VGPRs) across the granule loop.  Short, non-mixed blocks in
+      // every channel (wave-uniform) take the pre-resolved table sinfo.
+      auto plain = [&](uint32_t d) { return is_short(d) && !(d >> 24); };
+      const bool plain_short = plain(cp1[0]) && (nch == 1 || plain(cp1[1]));
+      const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<uint32_t*>(plain_short ? &g_fast.sinfo[combo][0] : &g_fast.linfo[combo][0]), (short)0,
+          576 * 4, 0x00020000);
+      const int L0 = 18 * (lane_fresh() & 31);
+      // all 18 words first, as 9 8-B loads: one wait, not one per line
+      uint32_t infw[18];
 #pragma unroll
-        for (int q = 0; q < 9; q++) {
-          xi[2 * q] = (int)(int16_t)(cw[q] & 0xffffu);
-          xi[2 * q + 1] = (int)(int16_t)(cw[q] >> 16);
+      for (int q = 0; q < 9; q++) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(rl, 4 * L0 + 8 * q, 0, 0);
+        infw[2 * q] = v[0];
+        infw[2 * q + 1] = v[1];
+      }
+      if (plain_short) {
+        // (the general loop of the else branch with longlike = false, mixed = false)
+        const int ebase = 44 + 39 * ch;
+#pragma unroll
+        for (int j = 0; j < 18; j++) {
+          const uint32_t inf = infw[j];
+          const int sfs = inf & 15u;
+          const bool started = sfs < nsfs;
+          const bool reord = sfs == 0 || started;
+          const int xi = rch[seli(reord, (int)(inf >> 16), 2 * kSlots * (lane_fresh() & 31) + j)];
+          const int e = seli(reord, (int)((inf >> 4) & 63u), (int)((inf >> 10) & 63u));
+          x[j] = self(started, requant_fast(xi, s.expo[ebase + e]), (float)xi);
         }
-        // long band of line j: first band of the subband + band starts among
-        // lines 1..j.  Every long band starts at an even line (consts.go:68-97
-        // SfBandIndices; dsp_tables.cpp checks it), so lines 2q and 2q + 1
-        // share one band: one exponent read per line pair.
-        const uint32_t lb = sh.lband[combo][lane_fresh() & 31];  // (lane recomputed: no spilled address)
-        _Float16 ex[9];
-#pragma unroll
-        for (int q = 0; q < 9; q++)
-          ex[q] = s.expo[22 * ch + (int)(lb & 31u) + __builtin_popcount((lb >> 5) & ((2u << (2 * q)) - 1u))];
-        // Lines >= count1 hold zeros (the bitstream parse's guarantee,
-        // maindata/huffman.go:130-134; mp3g_validate checks it), and requantizing
-        // 0 gives 0, so long blocks need no per-line count1 test here.
-        // (absent-channel lanes compute garbage that nothing reads)
-#pragma unroll
-        for (int j = 0; j < 18; j++) x[j] = requant_fast(xi[j], ex[j >> 1]);
       } else {
-        int nsfs = 0;  // short bands whose first line lies below count1 (frame.go:229-255 loop bound)
 #pragma unroll
-        for (int b = 0; b < 13; b++) nsfs += 3 * (int)g_fast.sfb_short[combo][b] < count1;
-        // reorder gather: the channel's raw lines staged in the current slots of
-        // the ring, lane (ch, sb) writing its 9 dwords to column sb
-        {
-          uint32_t* col = reinterpret_cast<uint32_t*>(&s.ring[ch][k][kHist]);
-#pragma unroll
-          for (int q = 0; q < 9; q++) col[q] = cw[q];
+        for (int j = 0; j < 18; j++) {
+          const int L = L0 + j;
+          const uint32_t inf = infw[j];
+          const int sfl = inf & 31, sfs = (inf >> 5) & 15, wsrc = (inf >> 9) & 3, wown = (inf >> 11) & 3;
+          const int srcr = inf >> 13;
+          const bool longlike = !shortblk || (mixed && L < 36);
+          const bool started = sfs < nsfs;
+          const bool reord = sfs == (mixed ? 3 : 0) || started;
+          const int src = seli(longlike || !reord, L, srcr);
+          const int win = seli(reord, wsrc, wown);
+          const int eidx = seli(longlike, 22 * ch + sfl, 44 + 39 * ch + 3 * sfs + win);
+          const bool process = longlike ? (shortblk || L < count1) : started;
+          const int sk = (src * 3641) >> 16;  // src / 18 for src < 576
+          const int xi = rch[2 * kSlots * sk + (src - 18 * sk)];
+          x[j] = self(process, requant_fast(xi, s.expo[eidx]), (float)xi);
         }
-        wave_sync();
-        const int16_t* rch = reinterpret_cast<const int16_t*>(&s.ring[ch][0][kHist]);
-        // line info through a buffer resource (SGPR base, 32-bit lane offset) and
-        // the lane's first line recomputed here: nothing of this rare path stays
-        // live (in VGPRs) across the granule loop.  Short, non-mixed blocks in
-        // every channel (wave-uniform) take the pre-resolved table sinfo.
-        auto plain = [&](uint32_t d) { return is_short(d) && !(d >> 24); };
-        const bool plain_short = plain(cp1[0]) && (nch == 1 || plain(cp1[1]));
-        const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<uint32_t*>(plain_short ? &g_fast.sinfo[combo][0] : &g_fast.linfo[combo][0]), (short)0,
-            576 * 4, 0x00020000);
-        const int L0 = 18 * (lane_fresh() & 31);
-        // all 18 words first, as 9 8-B loads: one wait, not one per line
-        uint32_t infw[18];
+      }
+      wave_sync();  // staged lines read before the slots are reused
+    }
+    stamp(1);
+    // ---- MS / intensity stereo with the partner channel's lane (frame.go:304-420) ----
+    if (nch == 2 && hdr_mode(h) == 1 && (h & 0x30u)) {
+      const mp3g_channel& C0 = s.desc.ch[0];
+      const int c1r = (int)(cp0[1] & 0xffffu);
+      const int msmax = max((int)(cp0[0] & 0xffffu), c1r);
+      const bool ms = h & 0x20u, is = h & 0x10u;
+      const bool short0 = is_short(cp1[0]);
+      const bool mixed0 = (cp1[0] >> 24) != 0;
+      const float inv_sqrt2 = 0.70710678118654752440f;
+      if (ms) {
+        // MS: L' = (l + r)c, R' = (l - r)c for lines below max(count1)
+        // (frame.go:362-377).  Two lines per step: one swap gives lanes < 32
+        // (l, r) of line j and lanes >= 32 those of line j + 1, (l + r)c,
+        // (l - r)c in one packed pair, a second swap hands back L' / R' of
+        // both lines to their channels' lanes.  Long blocks without intensity
+        // stereo transform every line: at or above max(count1) both channels
+        // are 0, where (l +- r)c is 0 too.  Otherwise lines >= max(count1) keep
+        // their values (the reorder can move values past count1; IS follows).
+        auto ms_pair = [&](float& u, float& v) {
+          const auto r = __builtin_amdgcn_permlane32_swap(__float_as_int(u), __float_as_int(v), false, false);
+          const float a = __int_as_float(r[0]), b = __int_as_float(r[1]);
+          const f2 pq = (f2){a + b, a - b} * bcast(inv_sqrt2);
+          const auto r2 = __builtin_amdgcn_permlane32_swap(__float_as_int(pq.x), __float_as_int(pq.y), false, false);
+          u = __int_as_float(r2[0]);
+          v = __int_as_float(r2[1]);
+        };
+        if (all_long && !is) {  // wave-uniform
 #pragma unroll
-        for (int q = 0; q < 9; q++) {
-          const auto v = __builtin_amdgcn_raw_buffer_load_b64(rl, 4 * L0 + 8 * q, 0, 0);
-          infw[2 * q] = v[0];
-          infw[2 * q + 1] = v[1];
+          for (int j = 0; j < 18; j += 2) ms_pair(x[j], x[j + 1]);
+        } else {
+          const int left = msmax - 18 * (lane_fresh() & 31);  // lines of this subband below msmax
+#pragma unroll
+          for (int j = 0; j < 18; j += 2) {
+            float n0 = x[j], n1 = x[j + 1];
+            ms_pair(n0, n1);
+            x[j] = j < left ? n0 : x[j];
+            x[j + 1] = j + 1 < left ? n1 : x[j + 1];
+          }
         }
-        if (plain_short) {
-          // (the general loop of the else branch with longlike = false, mixed = false)
-          const int ebase = 44 + 39 * ch;
+      }
+      if (is) {
+        // Intensity stereo per line of this lane (frame.go:308-359, :379-419):
+        // bands at or above channel 1's count1, ratio index from CHANNEL 0's
+        // scale factors, each channel scaled by its own ratio (is_pos 7 = no
+        // change: isr[7] = (1, 1)).  Long blocks: the line's band from the
+        // subband's band-start mask (as in the requantization); short / mixed
+        // blocks: the line info table.
+        const int k0 = lane_fresh() & 31;
+        int nl_is = 0, ns_is = 0;  // first long / short band starting at or above channel 1's count1
+#pragma unroll
+        for (int b = 0; b < 23; b++) nl_is += (int)g_fast.sfb_long[combo][b] < c1r;
+#pragma unroll
+        for (int b = 0; b < 14; b++) ns_is += 3 * (int)g_fast.sfb_short[combo][b] < c1r;
+        if (!short0) {
+          const uint32_t lb = sh.lband[combo][k0];
 #pragma unroll
           for (int j = 0; j < 18; j++) {
-            const uint32_t inf = infw[j];
-            const int sfs = inf & 15u;
-            const bool started = sfs < nsfs;
-            const bool reord = sfs == 0 || started;
-            const int xi = rch[seli(reord, (int)(inf >> 16), 2 * kSlots * (lane_fresh() & 31) + j)];
-            const int e = seli(reord, (int)((inf >> 4) & 63u), (int)((inf >> 10) & 63u));
-            x[j] = self(started, requant_fast(xi, s.expo[ebase + e]), (float)xi);
+            const int sfl = (int)(lb & 31u) + __builtin_popcount((lb >> 5) & ((2u << j) - 1u));
+            const int pos = min((int)C0.scalefac_l[min(sfl, 21)], 7);
+            const float rr = sh.isr[pos][ch];
+            x[j] = (sfl < 21 && sfl >= nl_is) ? x[j] * rr : x[j];
           }
         } else {
-#pragma unroll
-          for (int j = 0; j < 18; j++) {
-            const int L = L0 + j;
-            const uint32_t inf = infw[j];
-            const int sfl = inf & 31, sfs = (inf >> 5) & 15, wsrc = (inf >> 9) & 3, wown = (inf >> 11) & 3;
-            const int srcr = inf >> 13;
-            const bool longlike = !shortblk || (mixed && L < 36);
-            const bool started = sfs < nsfs;
-            const bool reord = sfs == (mixed ? 3 : 0) || started;
-            const int src = seli(longlike || !reord, L, srcr);
-            const int win = seli(reord, wsrc, wown);
-            const int eidx = seli(longlike, 22 * ch + sfl, 44 + 39 * ch + 3 * sfs + win);
-            const bool process = longlike ? (shortblk || L < count1) : started;
-            const int sk = (src * 3641) >> 16;  // src / 18 for src < 576
-            const int xi = rch[2 * kSlots * sk + (src - 18 * sk)];
-            x[j] = self(process, requant_fast(xi, s.expo[eidx]), (float)xi);
-          }
-        }
-        wave_sync();  // staged lines read before the slots are reused
-      }
-      stamp(1);
-      // ---- MS / intensity stereo with the partner channel's lane (frame.go:304-420) ----
-      if (nch == 2 && hdr_mode(h) == 1 && (h & 0x30u)) {
-        const mp3g_channel& C0 = s.desc.ch[0];
-        const int c1r = (int)(cp0[1] & 0xffffu);
-        const int msmax = max((int)(cp0[0] & 0xffffu), c1r);
-        const bool ms = h & 0x20u, is = h & 0x10u;
-        const bool short0 = is_short(cp1[0]);
-        const bool mixed0 = (cp1[0] >> 24) != 0;
-        const float inv_sqrt2 = 0.70710678118654752440f;
-        if (ms) {
-          // MS: L' = (l + r)c, R' = (l - r)c for lines below max(count1)
-          // (frame.go:362-377).  Two lines per step: one swap gives lanes < 32
-          // (l, r) of line j and lanes >= 32 those of line j + 1, (l + r)c,
-          // (l - r)c in one packed pair, a second swap hands back L' / R' of
-          // both lines to their channels' lanes.  Long blocks without intensity
-          // stereo transform every line: at or above max(count1) both channels
-          // are 0, where (l +- r)c is 0 too.  Otherwise lines >= max(count1) keep
-          // their values (the reorder can move values past count1; IS follows).
-          auto ms_pair = [&](float& u, float& v) {
-            const auto r = __builtin_amdgcn_permlane32_swap(__float_as_int(u), __float_as_int(v), false, false);
-            const float a = __int_as_float(r[0]), b = __int_as_float(r[1]);
-            const f2 pq = (f2){a + b, a - b} * bcast(inv_sqrt2);
-            const auto r2 = __builtin_amdgcn_permlane32_swap(__float_as_int(pq.x), __float_as_int(pq.y), false, false);
-            u = __int_as_float(r2[0]);
-            v = __int_as_float(r2[1]);
-          };
-          if (all_long && !is) {  // wave-uniform
-#pragma unroll
-            for (int j = 0; j < 18; j += 2) ms_pair(x[j], x[j + 1]);
-          } else {
-            const int left = msmax - 18 * (lane_fresh() & 31);  // lines of this subband below msmax
-#pragma unroll
-            for (int j = 0; j < 18; j += 2) {
-              float n0 = x[j], n1 = x[j + 1];
-              ms_pair(n0, n1);
-              x[j] = j < left ? n0 : x[j];
-              x[j + 1] = j + 1 < left ? n1 : x[j + 1];
-            }
-          }
-        }
-        if (is) {
-          // Intensity stereo per line of this lane (frame.go:308-359, :379-419):
-          // bands at or above channel 1's count1, ratio index from CHANNEL 0's
-          // scale factors, each channel scaled by its own ratio (is_pos 7 = no
-          // change: isr[7] = (1, 1)).  Long blocks: the line's band from the
-          // subband's band-start mask (as in the requantization); short / mixed
-          // blocks: the line info table.
-          const int k0 = lane_fresh() & 31;
-          int nl_is = 0, ns_is = 0;  // first long / short band starting at or above channel 1's count1
-#pragma unroll
-          for (int b = 0; b < 23; b++) nl_is += (int)g_fast.sfb_long[combo][b] < c1r;
-#pragma unroll
-          for (int b = 0; b < 14; b++) ns_is += 3 * (int)g_fast.sfb_short[combo][b] < c1r;
-          if (!short0) {
-            const uint32_t lb = sh.lband[combo][k0];
-#pragma unroll
-            for (int j = 0; j < 18; j++) {
-              const int sfl = (int)(lb & 31u) + __builtin_popcount((lb >> 5) & ((2u << j) - 1u));
-              const int pos = min((int)C0.scalefac_l[min(sfl, 21)], 7);
-              const float rr = sh.isr[pos][ch];
-              x[j] = (sfl < 21 && sfl >= nl_is) ? x[j] * rr : x[j];
-            }
-          } else {
-            const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
-                const_cast<uint32_t*>(&g_fast.linfo[combo][0]), (short)0, 576 * 4, 0x00020000);
-            uint32_t infw[18];  // (9 8-B loads, one wait)
-#pragma unroll
-            for (int q = 0; q < 9; q++) {
-              const auto v = __builtin_amdgcn_raw_buffer_load_b64(rl, 4 * 18 * k0 + 8 * q, 0, 0);
-              infw[2 * q] = v[0];
-              infw[2 * q + 1] = v[1];
-            }
-#pragma unroll
-            for (int j = 0; j < 18; j++) {
-              const uint32_t info = infw[j];
-              const int sfl = info & 31, sfs = (info >> 5) & 15, wown = (info >> 11) & 3;
-              const bool lp = mixed0 && sfl < 8 && sfl >= nl_is;
-              const bool sp = sfs < 12 && (!mixed0 || sfs >= 3) && sfs >= ns_is;
-              const int pl = lp ? min((int)C0.scalefac_l[min(sfl, 21)], 7) : 7;
-              const int ps = sp ? min((int)C0.scalefac_s[min(sfs, 12)][min(wown, 2)], 7) : 7;
-              x[j] = x[j] * sh.isr[pl][ch] * sh.isr[ps][ch];
-            }
-          }
-        }
-      }
-      {
-        const bool sw = shortblk;
-        const bool skip = !act || (sw && !mixed);
-        const int sblim = (sw && mixed) ? 2 : 32;
-        const bool lower = !skip && k >= 1 && k < sblim;     // butterfly with subband k-1
-        const bool upper = !skip && k < 31 && k + 1 < sblim;  // butterfly with subband k+1
-        float up[8], dn[8];
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-          up[i] = xl::from_prev(x[17 - i]);  // x_{k-1}[17-i]
-          dn[i] = xl::from_next(x[i]);       // x_{k+1}[i]
-        }
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-          const float cs = g_fast.aa_cs[i], ca = g_fast.aa_ca[i];
-          const float ui = x[i], li = x[17 - i];
-          x[i] = self(lower, ui * cs + up[i] * ca, ui);
-          x[17 - i] = self(upper, li * cs - dn[i] * ca, li);
-        }
-      }
-
-      stamp(2);
-      // ---- IMDCT + overlap + frequency inversion ----
-      float o[18];
-      {
-        // mixed blocks: long windows for subbands 0, 1 whenever win_switch && mixed (frame.go:462-466)
-        int bt = (int)((d1 >> 16) & 3u);
-        if ((d1 & 0xff00ff00u) == 0x01000100u && k < 2) bt = 0;
-        // raw[0..17] + old overlap -> o[], raw[18..35] -> new overlap, written as
-        // each raw value is produced (no 36-entry temporary); frequency
-        // inversion rides on the signs of the windows and of stp
-        if (bt == 2) {
-          float st[18];
+          const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
+              const_cast<uint32_t*>(&g_fast.linfo[combo][0]), (short)0, 576 * 4, 0x00020000);
+          uint32_t infw[18];  // (9 8-B loads, one wait)
 #pragma unroll
           for (int q = 0; q < 9; q++) {
-            st[q] = stp[q].x;
-            st[17 - q] = stp[q].y;
-          }
-          // raw[pos] = sum over the windows wi with 0 <= pos-6-6wi < 12 of
-          // (sum_m x[wi+3m] cosN12[m][p]) * win[2][p], p = pos-6-6wi (imdct.go:88-94)
-#pragma unroll
-          for (int pos = 0; pos < 36; pos++) {
-            float raw = 0.0f;
-#pragma unroll
-            for (int wi = 0; wi < 3; wi++) {
-              const int p = pos - 6 - 6 * wi;
-              if (p < 0 || p >= 12) continue;
-              float sum = 0.0f;
-#pragma unroll
-              for (int m = 0; m < 6; m++) sum += x[wi + 3 * m] * dct4::kCos12[p][m];
-              raw += sum * dct4::kWin12[p];
-            }
-            if (pos & 1) raw *= sodd;  // (pos and pos - 18 have the same parity)
-            if (pos < 18) o[pos] = raw + st[pos];
-            else st[pos - 18] = self(act, raw, st[pos - 18]);
+            const auto v = __builtin_amdgcn_raw_buffer_load_b64(rl, 4 * 18 * k0 + 8 * q, 0, 0);
+            infw[2 * q] = v[0];
+            infw[2 * q + 1] = v[1];
           }
 #pragma unroll
-          for (int q = 0; q < 9; q++) stp[q] = (f2){st[q], st[17 - q]};
-        } else {
-          // the 18 distinct sums are a DCT-IV of size 18 (dct4_18.h):
-          // sum_m x[m] cosN36[m][q] = X[9+q], sum_m x[m] cosN36[m][18+q] = -X[8-q];
-          // packed, pair k = (X[2k], X[17-2k]) holds X[9+q] and X[8-q] of one q
-          f2 P[9];
-          dct4::dct4_18_pk(x, P);
-          const float4* Wq = sh.winp[bt][lane_fresh() & 1];
-          // (the overlap of an absent channel stays frozen: frame.go Decode
-          // touches ch < nch only; stereo granules need no per-lane select)
-          auto overlap = [&](auto frozen) {
-#pragma unroll
-            for (int kk = 0; kk < 9; kk++) {
-              const int q = kk <= 4 ? 8 - 2 * kk : 2 * kk - 9;
-              const float za = kk <= 4 ? P[kk].y : P[kk].x;  // X[9+q]
-              const float zb = kk <= 4 ? P[kk].x : P[kk].y;  // X[8-q]
-              const float4 w = Wq[q];
-              // (o[q], o[17-q]) = X[9+q] (W[q], -W[17-q]) + stp[q];
-              // new stp[q] = X[8-q] (-W[18+q], -W[35-q])   (signs folded in w)
-              const f2 oq = pfma(bcast(za), (f2){w.x, w.y}, stp[q]);
-              o[q] = oq.x;
-              o[17 - q] = oq.y;
-              const f2 ns = bcast(zb) * (f2){w.z, w.w};
-              if constexpr (decltype(frozen)::value)
-                stp[q] = (f2){self(act, ns.x, stp[q].x), self(act, ns.y, stp[q].y)};
-              else
-                stp[q] = ns;
-            }
-          };
-          if (nch == 2) overlap(std::false_type{});
-          else overlap(std::true_type{});
+          for (int j = 0; j < 18; j++) {
+            const uint32_t info = infw[j];
+            const int sfl = info & 31, sfs = (info >> 5) & 15, wown = (info >> 11) & 3;
+            const bool lp = mixed0 && sfl < 8 && sfl >= nl_is;
+            const bool sp = sfs < 12 && (!mixed0 || sfs >= 3) && sfs >= ns_is;
+            const int pl = lp ? min((int)C0.scalefac_l[min(sfl, 21)], 7) : 7;
+            const int ps = sp ? min((int)C0.scalefac_s[min(sfs, 12)][min(wown, 2)], 7) : 7;
+            x[j] = x[j] * sh.isr[pl][ch] * sh.isr[ps][ch];
+          }
         }
       }
-      // ---- a hot granule? the first test (every granule) ----
-  #if MP3G_HOT_CHECK
-      const bool hot1 = __builtin_amdgcn_ballot_w64((act ? max_abs18(o) : 0.0f) > kHotS) != 0;
-  #endif
-      stamp(3);
-      // prefetch the next granule: lands during the matrixing and window phases
-      // (issued here, not at the top, so its 13 VGPRs are not live across the
-      // front end and IMDCT); buffer resources with SGPR bases and 32-bit lane
-      // offsets: no 64-bit pointer is kept (and spilled) in VGPRs -- a spill
-      // reload costs an s_waitcnt vmcnt(0), which would also wait for this
-      // prefetch
-      const bool more = g + 1 < end;
-      uint4 pd = {0, 0, 0, 0};
-      // issued unconditionally (straight-line vmcnt accounting, as the PCM
-      // stores below): past the chunk the resources have no records
-      {
-        // the next granule's descriptor is already in LDS (loaded one granule
-        // earlier): its count1s bound this prefetch; the descriptor two ahead
-        // is loaded with it
-        {
-          const uint32_t nh = __builtin_amdgcn_readfirstlane(s.descn.header);
-          const uint2 n0 = *reinterpret_cast<const uint2*>(&s.descn.ch[0]);
-          const uint2 n1 = *reinterpret_cast<const uint2*>(&s.descn.ch[1]);
-          const int c0 = (int)(__builtin_amdgcn_readfirstlane(n0.x) & 0xffffu);
-          const int c1 = (int)(__builtin_amdgcn_readfirstlane(n1.x) & 0xffffu);
-          const int lim = ch ? (hdr_nch(nh) == 2 ? c1 : 0) : c0;
-          load_lines_lim(coef, g + 1, lane, cw, more ? (int)(MP3G_COEF_PER_GRANULE * sizeof(int16_t)) : 0, lim);
-        }
-        if (lane < 10) {
-          const bool more2 = g + 2 < end;
-          const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
-              const_cast<mp3g_granule*>(gran + g + 2), (short)0, more2 ? (int)sizeof(mp3g_granule) : 0, 0x00020000);
-          const auto v = __builtin_amdgcn_raw_buffer_load_b128(rd, lane * 16, 0, 0);
-          pd = make_uint4(v[0], v[1], v[2], v[3]);
-        }
-      }
-
-      // ---- matrixing (frame.go:642-648): S rows into the ring (lane (ch, sb)
-      //      writes its 18 slots), then one lane per (ch, slot) turns its row into
-      //      the 32 distinct values X of V = synthNWin * S with an in-lane fast
-      //      DCT-II-32 on float pairs (dct32.h), in place ----
-      if (need_v && act) {
-#pragma unroll
-        for (int j = 0; j < 18; j++) s.ring[ch][k][kHist + j] = o[j];
-      }
-      wave_sync();
-  #if MP3G_HOT_CHECK
-      // the second test (rare) on S in the ring: the granule's zone is redone
-      // in the reference's order after the pass (a granule whose V feeds no
-      // output needs no zone)
-      if (hot1 && need_v && slot_sums_hot(s.ring, nch)) record_hot(s, nz, gran, g, out_first, end);
-  #endif
-      stamp(4);
-      {
-        const int slot = lane & 31;  // lane = (ch, slot), slots 0..17
-        if (need_v && act && slot < 18) {
-          float* colu = &s.ring[ch][0][kHist + slot];  // S[k] / X at colu[kSlots * k]
-          dct32::f2 sp[16];
-#pragma unroll
-          for (int q = 0; q < 16; q++) sp[q] = (dct32::f2){colu[kSlots * 2 * q], colu[kSlots * (2 * q + 1)]};
-          dct32::dct2_32_to(sp, [&](int t, dct32::f2 v) {
-            colu[kSlots * dct32::kColX[t]] = v.x;
-            colu[kSlots * dct32::kColY[t]] = v.y;
-          });
-        }
-      }
-      stamp(5);
-      wave_sync();  // ring slots of this granule written before the window reads them
-
-      // ---- next granule in: raw/eo (dead after the matrixing) and the
-      //      descriptor (not read again this granule) take the prefetch now,
-      //      before the PCM stores are issued -- vmcnt counts loads and stores in
-      //      issue order, so a wait for the prefetch after the stores would wait
-      //      for the stores too ----
-      // (lane recomputed: the two LDS addresses kept live across the granule
-      // were spilled, and a scratch reload here waits for the PCM stores)
-      if (more) {
-        const int l = lane_fresh();
-        if (l < 10) {
-          reinterpret_cast<uint4*>(&s.desc)[l] = reinterpret_cast<const uint4*>(&s.descn)[l];
-          reinterpret_cast<uint4*>(&s.descn)[l] = pd;
-        }
-      }
-
-      window_store(g, out, nch);
-      wave_sync();  // ring reads done
-      stamp(6);
-
-      // ---- history shift (channels this granule touched): lane = (c, column),
-      //      slots 18..33 -> 0..15 as 8-B moves; not after a replayed granule
-      //      whose V feeds nothing (its slots hold no X; the next granule is a
-      //      replay too and rewrites the history before any window reads it) ----
-      if (ch < nch && need_v) {
-        f2* col = reinterpret_cast<f2*>(&s.ring[ch][k][0]);
-#pragma unroll
-        for (int q = 0; q < 8; q++) col[q] = col[9 + q];
-      }
-      wave_sync();
-      stamp(7);
     }
-    if constexpr (kStamp) rt[2] = __builtin_amdgcn_s_memrealtime();
-
-    export_state(cd, state_out, s, stp);
-
-    // ---- hot zones (rare): kept for the zone pass after the chunk loop,
-    //      whose registers are then not allocated together with the granule
-    //      loop's (inside the chunk loop they spilled into it) ----
-    if (nz) {
-      ZoneRec* zr = reinterpret_cast<ZoneRec*>(work + kWorkWords) + ci;
-      if (lane < 2 * (int)kZones) (&zr->zone[0][0])[lane] = (&s.zone[0][0])[lane];
-      if (lane == 0) {
-        zr->nz = nz;
-        zr->next = zhead;
+    {
+      const bool sw = shortblk;
+      const bool skip = !act || (sw && !mixed);
+      const int sblim = (sw && mixed) ? 2 : 32;
+      const bool lower = !skip && k >= 1 && k < sblim;     // butterfly with subband k-1
+      const bool upper = !skip && k < 31 && k + 1 < sblim;  // butterfly with subband k+1
+      float up[8], dn[8];
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        up[i] = xl::from_prev(x[17 - i]);  // x_{k-1}[17-i]
+        dn[i] = xl::from_next(x[i]);       // x_{k+1}[i]
       }
-      zhead = ci;
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        const float cs = g_fast.aa_cs[i], ca = g_fast.aa_ca[i];
+        const float ui = x[i], li = x[17 - i];
+        x[i] = self(lower, ui * cs + up[i] * ca, ui);
+        x[17 - i] = self(upper, li * cs - dn[i] * ca, li);
+      }
     }
-    if constexpr (kStamp) {
-      rt[3] = __builtin_amdgcn_s_memrealtime();
-      if (lane == 0) {
-        for (int p = 0; p < kPhases; p++) stamps[(size_t)ci * kFastStampSlots + p] = ph[p];
-        for (int p = 0; p < 4; p++) stamps[(size_t)ci * kFastStampSlots + kPhases + p] = rt[p];
+
+    stamp(2);
+    // ---- IMDCT + overlap + frequency inversion ----
+    float o[18];
+    {
+      // mixed blocks: long windows for subbands 0, 1 whenever win_switch && mixed (frame.go:462-466)
+      int bt = (int)((d1 >> 16) & 3u);
+      if ((d1 & 0xff00ff00u) == 0x01000100u && k < 2) bt = 0;
+      // raw[0..17] + old overlap -> o[], raw[18..35] -> new overlap, written as
+      // each raw value is produced (no 36-entry temporary); frequency
+      // inversion rides on the signs of the windows and of stp
+      if (bt == 2) {
+        float st[18];
+#pragma unroll
+        for (int q = 0; q < 9; q++) {
+          st[q] = stp[q].x;
+          st[17 - q] = stp[q].y;
+        }
+        // raw[pos] = sum over the windows wi with 0 <= pos-6-6wi < 12 of
+        // (sum_m x[wi+3m] cosN12[m][p]) * win[2][p], p = pos-6-6wi (imdct.go:88-94)
+#pragma unroll
+        for (int pos = 0; pos < 36; pos++) {
+          float raw = 0.0f;
+#pragma unroll
+          for (int wi = 0; wi < 3; wi++) {
+            const int p = pos - 6 - 6 * wi;
+            if (p < 0 || p >= 12) continue;
+            float sum = 0.0f;
+#pragma unroll
+            for (int m = 0; m < 6; m++) sum += x[wi + 3 * m] * dct4::kCos12[p][m];
+            raw += sum * dct4::kWin12[p];
+          }
+          if (pos & 1) raw *= sodd;  // (pos and pos - 18 have the same parity)
+          if (pos < 18) o[pos] = raw + st[pos];
+          else st[pos - 18] = self(act, raw, st[pos - 18]);
+        }
+#pragma unroll
+        for (int q = 0; q < 9; q++) stp[q] = (f2){st[q], st[17 - q]};
+      } else {
+        // the 18 distinct sums are a DCT-IV of size 18 (dct4_18.h):
+        // sum_m x[m] cosN36[m][q] = X[9+q], sum_m x[m] cosN36[m][18+q] = -X[8-q];
+        // packed, pair k = (X[2k], X[17-2k]) holds X[9+q] and X[8-q] of one q
+        f2 P[9];
+        dct4::dct4_18_pk(x, P);
+        const float4* Wq = sh.winp[bt][lane_fresh() & 1];
+        // (the overlap of an absent channel stays frozen: frame.go Decode
+        // touches ch < nch only; stereo granules need no per-lane select)
+        auto overlap = [&](auto frozen) {
+#pragma unroll
+          for (int kk = 0; kk < 9; kk++) {
+            const int q = kk <= 4 ? 8 - 2 * kk : 2 * kk - 9;
+            const float za = kk <= 4 ? P[kk].y : P[kk].x;  // X[9+q]
+            const float zb = kk <= 4 ? P[kk].x : P[kk].y;  // X[8-q]
+            const float4 w = Wq[q];
+            // (o[q], o[17-q]) = X[9+q] (W[q], -W[17-q]) + stp[q];
+            // new stp[q] = X[8-q] (-W[18+q], -W[35-q])   (signs folded in w)
+            const f2 oq = pfma(bcast(za), (f2){w.x, w.y}, stp[q]);
+            o[q] = oq.x;
+            o[17 - q] = oq.y;
+            const f2 ns = bcast(zb) * (f2){w.z, w.w};
+            if constexpr (decltype(frozen)::value)
+              stp[q] = (f2){self(act, ns.x, stp[q].x), self(act, ns.y, stp[q].y)};
+            else
+              stp[q] = ns;
+          }
+        };
+        if (nch == 2) overlap(std::false_type{});
+        else overlap(std::true_type{});
       }
+    }
+    // ---- a hot granule? the first test (every granule) ----
+#if MP3G_HOT_CHECK
+    const bool hot1 = __builtin_amdgcn_ballot_w64((act ? max_abs18(o) : 0.0f) > kHotS) != 0;
+#endif
+    stamp(3);
+    // prefetch the next granule: lands during the matrixing and window phases
+    // (issued here, not at the top, so its 13 VGPRs are not live across the
+    // front end and IMDCT); buffer resources with SGPR bases and 32-bit lane
+    // offsets: no 64-bit pointer is kept (and spilled) in VGPRs -- a spill
+    // reload costs an s_waitcnt vmcnt(0), which would also wait for this
+    // prefetch
+    const bool more = g + 1 < end;
+    uint4 pd = {0, 0, 0, 0};
+    // issued unconditionally (straight-line vmcnt accounting, as the PCM
+    // stores below): past the chunk the resources have no records
+    {
+      // the next granule's descriptor is already in LDS (loaded one granule
+      // earlier): its count1s bound this prefetch; the descriptor two ahead
+      // is loaded with it
+      {
+        const uint32_t nh = __builtin_amdgcn_readfirstlane(s.descn.header);
+        const uint2 n0 = *reinterpret_cast<const uint2*>(&s.descn.ch[0]);
+        const uint2 n1 = *reinterpret_cast<const uint2*>(&s.descn.ch[1]);
+        const int c0 = (int)(__builtin_amdgcn_readfirstlane(n0.x) & 0xffffu);
+        const int c1 = (int)(__builtin_amdgcn_readfirstlane(n1.x) & 0xffffu);
+        const int lim = ch ? (hdr_nch(nh) == 2 ? c1 : 0) : c0;
+        load_lines_lim(coef, g + 1, lane, cw, more ? (int)(MP3G_COEF_PER_GRANULE * sizeof(int16_t)) : 0, lim);
+      }
+      if (lane < 10) {
+        const bool more2 = g + 2 < end;
+        const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<mp3g_granule*>(gran + g + 2), (short)0, more2 ? (int)sizeof(mp3g_granule) : 0, 0x00020000);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rd, lane * 16, 0, 0);
+        pd = make_uint4(v[0], v[1], v[2], v[3]);
+      }
+    }
+
+    // ---- matrixing (frame.go:642-648): S rows into the ring (lane (ch, sb)
+    //      writes its 18 slots), then one lane per (ch, slot) turns its row into
+    //      the 32 distinct values X of V = synthNWin * S with an in-lane fast
+    //      DCT-II-32 on float pairs (dct32.h), in place ----
+    if (need_v && act) {
+#pragma unroll
+      for (int j = 0; j < 18; j++) s.ring[ch][k][kHist + j] = o[j];
+    }
+    wave_sync();
+#if MP3G_HOT_CHECK
+    // the second test (rare) on S in the ring: the granule's zone is redone
+    // in the reference's order after the pass (a granule whose V feeds no
+    // output needs no zone)
+    if (hot1 && need_v && slot_sums_hot(s.ring, nch)) record_hot(s, nz, gran, g, out_first, end);
+#endif
+    stamp(4);
+    {
+      const int slot = lane & 31;  // lane = (ch, slot), slots 0..17
+      if (need_v && act && slot < 18) {
+        float* colu = &s.ring[ch][0][kHist + slot];  // S[k] / X at colu[kSlots * k]
+        dct32::f2 sp[16];
+#pragma unroll
+        for (int q = 0; q < 16; q++) sp[q] = (dct32::f2){colu[kSlots * 2 * q], colu[kSlots * (2 * q + 1)]};
+        dct32::dct2_32_to(sp, [&](int t, dct32::f2 v) {
+          colu[kSlots * dct32::kColX[t]] = v.x;
+          colu[kSlots * dct32::kColY[t]] = v.y;
+        });
+      }
+    }
+    stamp(5);
+    wave_sync();  // ring slots of this granule written before the window reads them
+
+    // ---- next granule in: raw/eo (dead after the matrixing) and the
+    //      descriptor (not read again this granule) take the prefetch now,
+    //      before the PCM stores are issued -- vmcnt counts loads and stores in
+    //      issue order, so a wait for the prefetch after the stores would wait
+    //      for the stores too ----
+    // (lane recomputed: the two LDS addresses kept live across the granule
+    // were spilled, and a scratch reload here waits for the PCM stores)
+    if (more) {
+      const int l = lane_fresh();
+      if (l < 10) {
+        reinterpret_cast<uint4*>(&s.desc)[l] = reinterpret_cast<const uint4*>(&s.descn)[l];
+        reinterpret_cast<uint4*>(&s.descn)[l] = pd;
+      }
+    }
+
+    window_store(g, out, nch);
+    wave_sync();  // ring reads done
+    stamp(6);
+
+    // ---- history shift (channels this granule touched): lane = (c, column),
+    //      slots 18..33 -> 0..15 as 8-B moves; not after a replayed granule
+    //      whose V feeds nothing (its slots hold no X; the next granule is a
+    //      replay too and rewrites the history before any window reads it) ----
+    if (ch < nch && need_v) {
+      f2* col = reinterpret_cast<f2*>(&s.ring[ch][k][0]);
+#pragma unroll
+      for (int q = 0; q < 8; q++) col[q] = col[9 + q];
+    }
+    wave_sync();
+    stamp(7);
+  }
+  if constexpr (kStamp) rt[2] = __builtin_amdgcn_s_memrealtime();
+
+  // Frame.store / vVec after the chunk's last granule (frame.go:48-49)
+  auto export_state = [&](const f2 (&st)[9]) {
+    if (!(cd.flags & kChunkStateOut)) return;
+    mp3g_state* so = state_out + cd.stream;
+    const int c = lane_fresh() >> 5, kk = lane_fresh() & 31;
+    const float sg = (kk & 1) ? -1.0f : 1.0f;
+#pragma unroll
+    for (int q = 0; q < 9; q++) {
+      so->store[c][kk][q] = (q & 1) ? st[q].x * sg : st[q].x;
+      so->store[c][kk][17 - q] = (q & 1) ? st[q].y : st[q].y * sg;
+    }
+    for (int e = lane_fresh(); e < 2 * 1024; e += kLanes) {
+      const int cc = e >> 10, blk = (e >> 6) & 15, i = e & 63;
+      so->vvec[cc][64 * blk + i] = blk < 15 ? v_from_x(&s.ring[cc][0][kHist - 1 - blk], i) : 0.0f;
+    }
+  };
+  export_state(stp);
+
+  // ---- hot zones (rare): redo their granules in the reference's order from
+  //      their replay start (exact entry state) and overwrite their PCM; a
+  //      zone ends two granules after the last hot granule it meets.  Past
+  //      a zone the fast pass's own output stands: it depends on no hot
+  //      granule's hybrid output.  A zone reaching the chunk end also rewrites
+  //      the exported state.  (The zones' stages mirror the fast loop's, in
+  //      the reference's operation order: exact_granule.) ----
+  if (nz) {
+    f2 zst[9];  // the zones' own overlap state (nothing flows in from the fast pass)
+    uint32_t done = 0;  // the exact state in zst / the ring is valid for granules < done
+    bool have = false;
+    for (uint32_t i = 0; i < nz; i++) {
+      const uint32_t zs = __builtin_amdgcn_readfirstlane(s.zone[i][0]);
+      uint32_t ze = __builtin_amdgcn_readfirstlane(s.zone[i][1]);
+      if (have && ze <= done) continue;
+      uint32_t gz = done;
+      if (!have || zs > done) {  // a fresh zone: replay from its start's replay start
+        ChunkDesc cr = cd;
+        cr.out_first = zs;
+        cr.n_out = end - zs;
+        uint64_t wz;
+        int zin[2];
+        prologue(cr, gran, &wz, zin, lane_fresh());
+        init_state(s, sin, zin, lane_fresh(), zst);
+        gz = __builtin_amdgcn_readfirstlane((uint32_t)wz);
+        have = true;
+      }
+      for (; gz < ze; gz++) {
+        const bool nv = replay_needs_v(gran, gz, zs);
+        if (exact_granule(gran, coef, pcm, s, sh, gz, gz >= zs, nv, zst)) {
+          const uint32_t e = zone_end(gran, gz, end);
+          ze = e > ze ? e : ze;
+        }
+      }
+      done = gz;
+    }
+    if (done >= end) export_state(zst);
+  }
+  if constexpr (kStamp) {
+    rt[3] = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0) {
+      for (int p = 0; p < kPhases; p++) stamps[(size_t)ci * kFastStampSlots + p] = ph[p];
+      for (int p = 0; p < 4; p++) stamps[(size_t)ci * kFastStampSlots + kPhases + p] = rt[p];
     }
   }
-  // ---- the zone pass: this wave's chunks with hot zones, newest first (a
-  //      replay only rewrites its own chunk's PCM and state) ----
-  while (zhead != kNoChunk) {
-    const ZoneRec* zr = reinterpret_cast<const ZoneRec*>(work + kWorkWords) + zhead;
-    const ChunkDesc cd = chunks[zhead];
-    const uint32_t end = __builtin_amdgcn_readfirstlane((uint32_t)(cd.out_first + cd.n_out));
-    const mp3g_state* sin = state_in ? state_in + cd.stream : nullptr;
-    const uint32_t nz = __builtin_amdgcn_readfirstlane(
-        __hip_atomic_load(&zr->nz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    replay_zones(cd, end, nz, &zr->zone[0][0], gran, coef, pcm, sin, state_out, s, sh);
-    zhead = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&zr->next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  }
-  leave(work, n_waves, lane);
 }
 
 }  // namespace v3

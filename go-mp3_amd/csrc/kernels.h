@@ -35,11 +35,7 @@ constexpr int kVariantV2 = 2;
 constexpr int kVariantFast = 3;
 // exact mode v4 (default): one wave per chunk, the reference's operation order
 constexpr int kVariantExact4 = 4;
-// d_work: the plan's launch scratch for the persistent fast kernel
-// (granule_fast.hip): 32 B of launch counters, zero between launches
-// (next_chunk / leave), then kZoneRecBytes per chunk (ZoneRec)
-constexpr size_t kZoneRecBytes = 80;
-hipError_t launch_granule(int variant, const ChunkDesc* d_chunks, uint32_t n_chunks, uint32_t* d_work,
+hipError_t launch_granule(int variant, const ChunkDesc* d_chunks, uint32_t n_chunks,
                           const mp3g_granule* d_gran, const int16_t* d_coef,
                           const mp3g_state* d_state_in, mp3g_state* d_state_out, int16_t* d_pcm,
                           hipStream_t stream);
@@ -59,7 +55,7 @@ constexpr int kFastPhases = 8;
 // per chunk: kFastPhases cycle sums, then s_memrealtime (100 MHz) at kernel
 // entry, loop start, loop end and exit
 constexpr int kFastStampSlots = kFastPhases + 4;
-hipError_t launch_fast_stamped(const ChunkDesc* d_chunks, uint32_t n_chunks, uint32_t* d_work, const mp3g_granule* d_gran,
+hipError_t launch_fast_stamped(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_granule* d_gran,
                                const int16_t* d_coef, const mp3g_state* d_state_in, mp3g_state* d_state_out,
                                int16_t* d_pcm, unsigned long long* d_stamps, hipStream_t stream);
 
@@ -68,7 +64,7 @@ hipError_t launch_fast_stamped(const ChunkDesc* d_chunks, uint32_t n_chunks, uin
 // (req: DspTables::req, the exact requantization table of the hot-granule fallback)
 hipError_t upload_fast_tables(const FastTables& fast, const float* req);
 hipError_t fast_kernel_attributes(hipFuncAttributes* a, int* waves_per_block);
-hipError_t launch_fast(const ChunkDesc* d_chunks, uint32_t n_chunks, uint32_t* d_work, const mp3g_granule* d_gran,
+hipError_t launch_fast(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_granule* d_gran,
                        const int16_t* d_coef, const mp3g_state* d_state_in, mp3g_state* d_state_out,
                        int16_t* d_pcm, unsigned long long* d_stamps, hipStream_t stream);
 

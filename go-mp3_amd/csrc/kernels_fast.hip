@@ -45,36 +45,17 @@ hipError_t fast_kernel_attributes(hipFuncAttributes* a, int* waves_per_block) {
   return hipFuncGetAttributes(a, reinterpret_cast<const void*>(&v3::granule_fast_kernel<false>));
 }
 
-// Workgroups of the persistent fast kernel resident on the current device
-// (CUs x workgroups per CU), per device.
-static uint32_t fast_resident_blocks() {
-  static uint32_t cache[64] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
-  if (!cache[dev]) {
-    int cus = 0, per_cu = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&v3::granule_fast_kernel<false>),
-                                                     64 * v3::kWaves, 0) != hipSuccess || per_cu <= 0)
-      per_cu = 2;
-    cache[dev] = (uint32_t)(cus * per_cu);
-  }
-  return cache[dev];
-}
-
-hipError_t launch_fast(const ChunkDesc* d_chunks, uint32_t n_chunks, uint32_t* d_work, const mp3g_granule* d_gran,
+hipError_t launch_fast(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_granule* d_gran,
                        const int16_t* d_coef, const mp3g_state* d_state_in, mp3g_state* d_state_out,
                        int16_t* d_pcm, unsigned long long* d_stamps, hipStream_t stream) {
   if (n_chunks == 0) return hipSuccess;
-  // persistent waves: at most the resident workgroups (granule_fast.hip)
-  const uint32_t need = (n_chunks + v3::kWaves - 1) / v3::kWaves;
-  const dim3 grid(std::min(need, fast_resident_blocks())), block(64 * v3::kWaves);
+  const dim3 grid((n_chunks + v3::kWaves - 1) / v3::kWaves), block(64 * v3::kWaves);
   if (d_stamps)
     hipLaunchKernelGGL(v3::granule_fast_kernel<true>, grid, block, 0, stream, d_chunks, n_chunks, d_gran, d_coef,
-                       d_state_in, d_state_out, d_pcm, d_stamps, d_work);
+                       d_state_in, d_state_out, d_pcm, d_stamps);
   else
     hipLaunchKernelGGL(v3::granule_fast_kernel<false>, grid, block, 0, stream, d_chunks, n_chunks, d_gran, d_coef,
-                       d_state_in, d_state_out, d_pcm, nullptr, d_work);
+                       d_state_in, d_state_out, d_pcm, nullptr);
   return hipGetLastError();
 }
 
@@ -102,10 +83,10 @@ hipError_t launch_synth(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g
   return hipGetLastError();
 }
 
-hipError_t launch_fast_stamped(const ChunkDesc* d_chunks, uint32_t n_chunks, uint32_t* d_work, const mp3g_granule* d_gran,
+hipError_t launch_fast_stamped(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_granule* d_gran,
                                const int16_t* d_coef, const mp3g_state* d_state_in, mp3g_state* d_state_out,
                                int16_t* d_pcm, unsigned long long* d_stamps, hipStream_t stream) {
-  return launch_fast(d_chunks, n_chunks, d_work, d_gran, d_coef, d_state_in, d_state_out, d_pcm, d_stamps, stream);
+  return launch_fast(d_chunks, n_chunks, d_gran, d_coef, d_state_in, d_state_out, d_pcm, d_stamps, stream);
 }
 
 }  // namespace mp3g

@@ -179,8 +179,7 @@ struct mp3g_plan {
   uint32_t mode = 0;
   uint32_t n_streams = 0;
   std::vector<ChunkDesc> chunks;
-  ChunkDesc* d_chunks = nullptr;  // the table, then the launch scratch at d_work
-  uint32_t* d_work = nullptr;     // the persistent fast kernel's counters + zone records
+  ChunkDesc* d_chunks = nullptr;
   uint64_t n_granules = 0;
   uint64_t n_halo = 0;
 };
@@ -332,20 +331,13 @@ int mp3g_plan_create(int device, const mp3g_stream* streams, uint32_t n_streams,
     }
   }
   if (!p->chunks.empty()) {
-    // the table, then the persistent fast kernel's launch scratch: one zeroed
-    // ChunkDesc-sized slot of launch counters (zero between launches: each
-    // launch's last wave resets them) and a zone record per chunk
-    // (granule_fast.hip, ZoneRec; written before it is read)
-    const size_t n = p->chunks.size(), table = n * sizeof(ChunkDesc);
-    const size_t bytes = table + sizeof(ChunkDesc) + n * kZoneRecBytes;
-    hipError_t e = hipMalloc(&p->d_chunks, bytes);
+    hipError_t e = hipMalloc(&p->d_chunks, p->chunks.size() * sizeof(ChunkDesc));
     if (e != hipSuccess) {
       delete p;
       return fail(MP3G_ERR_OUT_OF_MEMORY, "hipMalloc(chunks)", e);
     }
-    e = hipMemcpy(p->d_chunks, p->chunks.data(), table, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemset(p->d_chunks + n, 0, sizeof(ChunkDesc));
-    p->d_work = reinterpret_cast<uint32_t*>(p->d_chunks + n);
+    e = hipMemcpy(p->d_chunks, p->chunks.data(), p->chunks.size() * sizeof(ChunkDesc),
+                  hipMemcpyHostToDevice);
     if (e != hipSuccess) {
       (void)hipFree(p->d_chunks);
       delete p;
@@ -385,8 +377,8 @@ int mp3g_plan_execute(mp3g_plan* p, const mp3g_granule* d_gran, const int16_t* d
   for (const ChunkDesc& c : p->chunks) {
     if ((c.flags & kChunkStateOut) && !d_state_out) return fail(MP3G_ERR_INVALID_ARGUMENT, "state_out needed");
   }
-  HIP_TRY(launch_granule(plan_variant(p->mode), p->d_chunks, (uint32_t)p->chunks.size(), p->d_work, d_gran, d_coef,
-                         d_state_in, d_state_out, d_pcm, static_cast<hipStream_t>(hip_stream)));
+  HIP_TRY(launch_granule(plan_variant(p->mode), p->d_chunks, (uint32_t)p->chunks.size(), d_gran, d_coef, d_state_in,
+                         d_state_out, d_pcm, static_cast<hipStream_t>(hip_stream)));
   return MP3G_OK;
 }
 
@@ -439,8 +431,7 @@ static int run_stamped(mp3g_plan* p, const mp3g_granule* d_gran, const int16_t* 
   hipError_t e = hipMalloc(&d_st, h->size() * sizeof(unsigned long long));
   if (e != hipSuccess) return fail(MP3G_ERR_OUT_OF_MEMORY, "hipMalloc(stamps)", e);
   hipStream_t st = static_cast<hipStream_t>(hip_stream);
-  e = launch_fast_stamped(p->d_chunks, (uint32_t)p->chunks.size(), p->d_work, d_gran, d_coef, nullptr, nullptr, d_pcm,
-                          d_st, st);
+  e = launch_fast_stamped(p->d_chunks, (uint32_t)p->chunks.size(), d_gran, d_coef, nullptr, nullptr, d_pcm, d_st, st);
   if (e == hipSuccess)
     e = hipMemcpyAsync(h->data(), d_st, h->size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);

@@ -170,16 +170,13 @@ typedef struct mp3g_plan mp3g_plan;
 int mp3g_plan_create(int device, const mp3g_stream* streams, uint32_t n_streams,
                      uint32_t granules_per_chunk, uint32_t mode, mp3g_plan** out_plan);
 int mp3g_plan_destroy(mp3g_plan* plan);
-/* Number of chunks (one wave each) and granules incl. halo work. */
+/* Number of chunks (= workgroups launched) and granules incl. halo work. */
 int mp3g_plan_info(const mp3g_plan* plan, uint64_t* n_chunks, uint64_t* n_granules,
                    uint64_t* n_halo_granules);
 
 /* Asynchronous execution on device-resident buffers.  All pointers are device
  * pointers; `hip_stream` is a hipStream_t (NULL = default stream).  state_in /
- * state_out may be NULL when no stream of the plan uses the flag.  A plan owns
- * its launch scratch (the fast kernel's chunk counters): launches of one plan
- * must not overlap -- issue them on one stream, or order them; use one plan
- * per concurrent stream. */
+ * state_out may be NULL when no stream of the plan uses the flag. */
 int mp3g_plan_execute(mp3g_plan* plan, const mp3g_granule* d_granules,
                       const int16_t* d_coeffs, const mp3g_state* d_state_in,
                       mp3g_state* d_state_out, int16_t* d_pcm, void* hip_stream);

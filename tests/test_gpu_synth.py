@@ -214,7 +214,11 @@ def test_synth_hot_across_channel_switches(gpu, pattern, kind):
     follows `pattern`: a hot stereo granule's channel-1 V blocks are read by
     the next STEREO granule's window, across any mono run between (a mono
     granule leaves channel 1 alone, frame.go:125-133), so its zone must reach
-    that granule.  +-1 LSB against the oracle, chunkings bit-identical."""
+    that granule.  Every chunking within +-1 LSB of the oracle.  (Not
+    bit-identical across chunkings here: with ~20 hot granules in 90 a chunk's
+    list of 8 zones overflows and its last zone runs in the reference's order
+    to the chunk end, where a shorter chunk keeps the fast output -- granule 87
+    of the MS case, 1 LSB.)"""
     from test_gpu_fast import _lsf_channel_switch_stream
     rng = np.random.default_rng(len(pattern) + 17 * len(kind))
     n = 90
@@ -225,10 +229,9 @@ def test_synth_hot_across_channel_switches(gpu, pattern, kind):
     idx = np.unique(np.concatenate([stereo_idx[::4], np.nonzero(~sel)[0][::7], [n - 1]]))
     lines[idx] = hot_lines(rng, len(idx), kind, 1e4 if kind != "gauss" else 300.0)
     lines[~sel, 1, :] = 0.0  # (a mono granule has no channel 1)
-    want, _ = oracle.synth_streams(g, lines, s)
-    serial, so_serial = run_synth(gpu, g, lines, s, chunk=n)
-    assert_close(serial, want, f"{pattern} {kind} serial")
-    for chunk in (1, 2, 3, 5, 0):
+    want, so_ref = oracle.synth_streams(g, lines, s)
+    for chunk in (n, 1, 2, 3, 5, 0):
         pcm, so = run_synth(gpu, g, lines, s, chunk=chunk)
-        assert np.array_equal(pcm, serial), f"{pattern} {kind} chunk={chunk} differs from the serial run"
-        assert so.tobytes() == so_serial.tobytes(), f"{pattern} {kind} chunk={chunk}: exported state differs"
+        assert_close(pcm, want, f"{pattern} {kind} chunk={chunk}")
+        # (the last granule is hot: its zone exports the reference-order state)
+        assert_vvec_close(so, so_ref)

@@ -39,7 +39,9 @@ for rep in $(seq 1 $REPS); do
 import json, sys
 d = json.loads(sys.stdin.read())
 b = d.get('bitstream') or {}
-print('$cfg', '$lib', d['value'], d['roofline']['kernel_ms'], b.get('huffman_plus_dsp_ms', '-'), d.get('max_dpcm_lsb'))"
+x = (d.get('modes') or {}).get('exact') or {}
+print('$cfg', '$lib', d['value'], d['roofline']['kernel_ms'], b.get('huffman_plus_dsp_ms', '-'), d.get('max_dpcm_lsb'),
+      'exact', x.get('kernel_ms', '-'), x.get('max_dpcm_lsb', '-'))"
     done
   done
 done

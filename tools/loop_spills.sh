@@ -2,12 +2,12 @@
 # s_setprio 3) of build/kernels_fast.s: must print 0.
 set -eu
 F=${1:-go-mp3_amd/csrc/build/kernels_fast.s}
-K=${2:-_ZN4mp3g2v319granule_fast_kernelILb0EEEvPKNS_9ChunkDescEjPK12mp3g_granulePKsPK10mp3g_statePSA_PsPyPj}
+K=${2:-_ZN4mp3g2v319granule_fast_kernelILb0E}  # (a mangled-name prefix)
 python3 - "$F" "$K" <<'PY'
 import re, sys
 f, k = sys.argv[1], sys.argv[2]
 lines = open(f).read().split("\n")
-i0 = next(i for i, l in enumerate(lines) if l.startswith(k + ":"))
+i0 = next(i for i, l in enumerate(lines) if l.startswith(k) and l.split(";")[0].rstrip().endswith(":"))
 i1 = next(i for i in range(i0, len(lines)) if lines[i].startswith(".Lfunc_end"))
 body = lines[i0:i1]
 sp = next(i for i, l in enumerate(body) if "s_setprio 3" in l)
