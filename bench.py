@@ -60,7 +60,8 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=10,
+                    help="untimed steps first (the clock takes ~6 launches of c3 to settle)")
     ap.add_argument("--config", choices=["c2", "c3", "c5"], default="c3")
     ap.add_argument("--c5-copies", type=int, default=256,
                     help="c5: copies of each reference sample stream per GPU")
@@ -354,7 +355,7 @@ def polyphase_leg(args, rank, dev, stream, d_g, streams, n_gran, local):
     return out
 
 
-PROFILE_TAG = "r03g"  # profiles/<tag>_<cfg>_<kernel>.json of the current kernels
+PROFILE_TAG = "r04"  # profiles/<tag>_<cfg>_<kernel>.json of the current kernels
 
 
 def profiled_issue(cfg, kernel):

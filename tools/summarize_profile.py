@@ -23,6 +23,8 @@ import shutil
 import sys
 
 KERNEL = "granule"
+HEAD_STEPS = 20  # tools/profile.sh: the head pass times 20 steps
+TRACE_STEPS = {"c2": 20, "c3": 5}  # and the whole-bench passes these
 CALIB = {  # tools/flop_calib kernels: f32 flops per lane-instruction by the usual convention
     "calib_fma_f32": 2, "calib_add_f32": 1, "calib_mul_f32": 1, "calib_exp_f32": 1,
     "calib_pk_fma_f32": 4, "calib_pk_mul_f32": 2, "calib_pk_add_f32": 2}
@@ -96,9 +98,15 @@ def main(src, tag, cfg, dst="profiles", bytes_per_launch=None, kernel=None, suff
     k = [r for r in stats if kernel in r["Name"]][0]
     grid, durs = full_launches(base + "_head", kernel)
     dur_src = "head"
+    n_head = len(durs)
+    # the head pass is bench.py --steps 20: its last 20 launches are the timed
+    # ones (the first launches of a process run slower while the clock ramps)
+    durs = durs[-HEAD_STEPS:]
     if not durs:
         grid, durs = full_launches(base + "_trace", kernel)
         dur_src = "trace"
+        n_head = len(durs)
+        durs = durs[-TRACE_STEPS[cfg]:] if cfg in TRACE_STEPS else durs
     fetch = counters(base + "_fetch", kernel, grid).get("FETCH_SIZE")
     write = counters(base + "_write", kernel, grid).get("WRITE_SIZE")
     sq = counters(base + "_sq", kernel, grid)
@@ -111,7 +119,8 @@ def main(src, tag, cfg, dst="profiles", bytes_per_launch=None, kernel=None, suff
     if durs:
         avg_ns = sum(durs) / len(durs)
         out.update(grid=grid, calls=len(durs), avg_ns=avg_ns, min_ns=min(durs), max_ns=max(durs),
-                   duration_source=f"{dur_src} pass: rocprofv3 --kernel-trace, no counters, launches of grid {grid}")
+                   duration_source=f"{dur_src} pass: rocprofv3 --kernel-trace, no counters, launches of grid {grid}" +
+                   f" (the timed {len(durs)} of {n_head})")
     else:
         avg_ns = float(k["AverageNs"])
         out.update(calls=int(k["Calls"]), avg_ns=avg_ns, min_ns=float(k["MinNs"]), max_ns=float(k["MaxNs"]))
