@@ -132,7 +132,12 @@ def main():
     ap.add_argument("--granules", type=int, default=8192, help="per batch and pattern")
     ap.add_argument("--out", default=None)
     ap.add_argument("--only", default=None, help="synth | fused")
+    ap.add_argument("--hot-s", type=float, default=HOT_S,
+                    help="kHotS of the library under test (a build with -DMP3G_HOT_S=..., loaded via MP3G_LIB)")
+    ap.add_argument("--hot-l1", type=float, default=HOT_L1, help="kHotL1 of the library under test")
     args = ap.parse_args()
+    global HOT_S, HOT_L1
+    HOT_S, HOT_L1 = args.hot_s, args.hot_l1
     import torch  # noqa: F401  (shared HIP runtime)
     import mp3g
     import oracle
