@@ -313,10 +313,13 @@ __device__ __forceinline__ float v_from_x(const float* x, int i) {
 // entry state that is itself exact: a zone replays the granules that state
 // depends on from its replay start (the chunk-halo rule: S_g needs x_{g-1}'s
 // overlap, V_{g-1} needs x_{g-2}'s).
-// Below kHotS the fast transforms stay within +-1 LSB with a 4-8x margin in
-// magnitude (tools/fast_tolerance.py, DESIGN.md "Fast mode on every valid input").
+// Below kHotS the fast transforms stay within +-1 LSB: an adversarial search
+// that drives every line of a granule to just under the bound (dense random
+// signs, rows of synthNWin, alternating subbands, tools/adversarial_tolerance.py)
+// found 2 LSB at a bound of 8 (the standalone polyphase kernel) and at most 1
+// at 6 and at 4; 4 is kept (DESIGN.md "Fast mode on every valid input").
 #ifndef MP3G_HOT_S
-#define MP3G_HOT_S 8.0f
+#define MP3G_HOT_S 4.0f
 #endif
 constexpr float kHotS = MP3G_HOT_S;
 #ifndef MP3G_HOT_CHECK
@@ -329,8 +332,8 @@ constexpr float kHotS = MP3G_HOT_S;
 // granule of the synthetic c3 streams) do not, and the fast transforms are
 // measured within +-1 LSB on those up to |S| = 56 (tools/fast_tolerance.py,
 // spike patterns).  So a granule is hot when max |S| > kHotS (all lines at
-// most 8: per-slot sums <= 256, measured within +-1 LSB on dense patterns)
-// AND some slot's sum exceeds kHotL1 (|X| <= 64 otherwise).
+// most 4: per-slot sums <= 128, within +-1 LSB on the adversarial dense
+// patterns) AND some slot's sum exceeds kHotL1 (|X| <= 64 otherwise).
 #ifndef MP3G_HOT_L1
 #define MP3G_HOT_L1 64.0f
 #endif

@@ -270,6 +270,11 @@ def scan_streams(datas, n_threads=0):
 
 
 HUFF_ROWS_COUNT1 = 1  # mp3g_huffman_execute_ex: rows written only up to count1 (+ padding)
+# fast mode's magnitude bounds (granule_fast.hip kHotS / kHotL1, checked by
+# tests/test_abi_cpu.py): a granule with max |S| > FAST_HOT_S and a time slot
+# whose sum of |S| over the 32 subbands exceeds FAST_HOT_L1 runs in the
+# reference's operation order
+FAST_HOT_S, FAST_HOT_L1 = 4.0, 64.0
 
 
 def huffman_execute(d_jobs, n_granules, d_main_data, d_granules, d_coeffs, stream=None, device=0, flags=0):

@@ -185,3 +185,12 @@ def test_host_output_buffers_are_checked():
     assert nb == 3 * 2304
     ptr, nb = mp3g._host_buffer(torch.zeros(100, dtype=torch.uint8), want_int16=False)
     assert nb == 100
+
+
+def test_fast_mode_bounds_match_the_kernel():
+    """mp3g.FAST_HOT_S / FAST_HOT_L1 (the tests' and tools' copy) are the
+    bounds the fast kernels are built with (granule_fast.hip defaults)."""
+    src = open(os.path.join(REPO, "go-mp3_amd", "csrc", "granule_fast.hip")).read()
+    s = float(re.search(r"#define MP3G_HOT_S ([0-9.]+)f", src).group(1))
+    l1 = float(re.search(r"#define MP3G_HOT_L1 ([0-9.]+)f", src).group(1))
+    assert (s, l1) == (mp3g.FAST_HOT_S, mp3g.FAST_HOT_L1)

@@ -139,7 +139,7 @@ def hot_lines(rng, n, kind, scale):
 
 @pytest.mark.parametrize("kind", ["alt", "altsb", "randsign", "gauss"])
 def test_synth_hot_granules(gpu, kind):
-    """Granules far above the fast transforms' magnitude bound (kHotS = 8)
+    """Granules far above the fast transforms' magnitude bound (kHotS)
     scattered through normal ones, isolated and in runs, at chunk starts and
     stream ends: max |dPCM| <= 1 against the oracle, bit-identical across
     chunkings, exported vVec close to the reference's."""
@@ -171,10 +171,45 @@ def test_synth_just_below_bound(gpu, kind):
     rng = np.random.default_rng(100 + len(kind))
     g, c, s = synth.synth_batch(4, 60, seed=91)
     lines = hot_lines(rng, len(g), kind, 1.0)
-    lines *= 0.95 * 8.0 / np.abs(lines).max(axis=(1, 2), keepdims=True)
+    lines *= 0.95 * gpu.FAST_HOT_S / np.abs(lines).max(axis=(1, 2), keepdims=True)
     want, _ = oracle.synth_streams(g, lines, s)
     got, _ = run_synth(gpu, g, lines, s)
     assert_close(got, want, f"{kind} at 0.95 kHotS")
+
+
+def _nwin_row_lines(rng, n, coherent):
+    """[n, 2, 576] lines whose every time slot is one row of synthNWin (up to
+    sign): the whole slot sum lands on one DCT output -- the shape that
+    maximised the fast transforms' error (tools/adversarial_tolerance.py)."""
+    nwin = oracle.tables()["synth_nwin"]
+    rows = np.sign(nwin[16:48])
+    m = rng.integers(0, 32, size=(n, 2))
+    sign = np.ones((n, 2, 1, 18)) if coherent else rng.choice([-1.0, 1.0], size=(n, 2, 1, 18))
+    S = rows[m][..., None] * sign  # [n, 2, 32 subbands, 18 slots]
+    return np.ascontiguousarray(S.reshape(n, 2, 576), dtype=np.float32)
+
+
+@pytest.mark.parametrize("kind", ["randsign", "nwin_row", "nwin_row_coherent"])
+@pytest.mark.parametrize("level", ["below", "old_bound"])
+def test_synth_adversarial_dense(gpu, kind, level):
+    """Every line of every granule at the magnitude limit (|S| = bound x
+    (1 - 1e-6)) in the adversarial search's worst shapes: dense random signs
+    and rows of synthNWin.  At kHotS = 8 (round 3) these reached 2 LSB on the
+    fast transforms; now `below` (just under kHotS = 4) stays fast and within
+    +-1 LSB, and `old_bound` (just under 8) is hot -- slot sums of 32 x 8 --
+    and runs in the reference's order."""
+    rng = np.random.default_rng(300 + len(kind) + len(level))
+    g, c, s = synth.synth_batch(4, 64, seed=95)
+    n = len(g)
+    if kind == "randsign":
+        lines = rng.choice([-1.0, 1.0], size=(n, 2, 576)).astype(np.float32)
+    else:
+        lines = _nwin_row_lines(rng, n, kind.endswith("coherent"))
+    bound = gpu.FAST_HOT_S if level == "below" else 8.0
+    lines *= np.float32(bound * (1.0 - 1e-6))
+    want, _ = oracle.synth_streams(g, lines, s)
+    got, _ = run_synth(gpu, g, lines, s)
+    assert_close(got, want, f"{kind} {level}")
 
 
 def test_synth_empty_plan_and_errors(gpu):

@@ -2,9 +2,9 @@
 """Adversarial search for the fast mode's worst |dPCM| just under the hot-granule
 thresholds (DESIGN.md "Fast mode on every valid input").
 
-A granule stays on the fast transforms when max |S| <= kHotS (8) or, above
-that, when every time slot's sum of |S| over the 32 subbands is <= kHotL1
-(64).  This drives inputs to those limits -- not 0.95 of them -- in the
+A granule stays on the fast transforms when max |S| <= kHotS (4; 8 until
+round 4, where this search found 2 LSB) or, above that, when every time
+slot's sum of |S| over the 32 subbands is <= kHotL1 (64).  This drives inputs to those limits -- not 0.95 of them -- in the
 shapes that maximise rounding error: coherent signs (S along a row of
 synthNWin, so one DCT output takes the whole slot sum), single-slot
 concentration, alternating subbands, sparse spikes of L1 = 64 split over
@@ -33,7 +33,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in ("go-mp3_amd", "oracle", "tests"):
     sys.path.insert(0, os.path.join(REPO, p))
 
-HOT_S, HOT_L1 = 8.0, 64.0
+HOT_S, HOT_L1 = 4.0, 64.0  # granule_fast.hip kHotS / kHotL1 (round 3: kHotS = 8)
 EDGE = 1.0 - 1e-6  # just under the limit
 
 
@@ -127,6 +127,7 @@ def measure(got, want):
 
 
 def main():
+    global HOT_S, HOT_L1
     ap = argparse.ArgumentParser()
     ap.add_argument("--batches", type=int, default=6)
     ap.add_argument("--granules", type=int, default=8192, help="per batch and pattern")
@@ -136,7 +137,6 @@ def main():
                     help="kHotS of the library under test (a build with -DMP3G_HOT_S=..., loaded via MP3G_LIB)")
     ap.add_argument("--hot-l1", type=float, default=HOT_L1, help="kHotL1 of the library under test")
     args = ap.parse_args()
-    global HOT_S, HOT_L1
     HOT_S, HOT_L1 = args.hot_s, args.hot_l1
     import torch  # noqa: F401  (shared HIP runtime)
     import mp3g
