@@ -475,7 +475,7 @@ def time_plan(mp3g, streams, d_g, d_c, d_pcm, mode, chunk, local, steps, warmup,
     for _ in range(warmup):
         plan.execute(d_g, d_c, d_pcm, stream=h)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -485,7 +485,7 @@ def time_plan(mp3g, streams, d_g, d_c, d_pcm, mode, chunk, local, steps, warmup,
         plan.execute(d_g, d_c, d_pcm, stream=h)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
@@ -571,7 +571,10 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     # (device_count does not initialise the GPU on this image)
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
-    if world > 1:
+    # a process group whenever torch.distributed.run started us, N = 1
+    # included: the RCCL path (barriers, device max over ranks, the gather)
+    # then runs on a one-GPU box too (tests/test_gpu_bench_dist.py)
+    if world > 1 or "WORLD_SIZE" in os.environ:
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
         else:
@@ -652,7 +655,7 @@ def main():
         del d_g2, d_c2, d_p2
 
     gather = None
-    if world > 1 and not args.no_gather:
+    if dist.is_initialized() and not args.no_gather:
         gather = gather_leg(args, rank, world, dev, d_pcm, n_gran, mdist)
 
     if rank == 0:
@@ -820,7 +823,7 @@ def main():
                 out["modes"][m]["max_dpcm_lsb"] = dpcm(r["pcm"], ref)
             out["max_dpcm_lsb"] = out["modes"][args.mode]["max_dpcm_lsb"]
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

@@ -4,8 +4,11 @@ The driver runs `bench.py --gpus N` under torch.distributed.run on a whole
 8-GPU node with RCCL; that branch (process group, barriers, max over ranks,
 the timed PCM gather to rank 0 into one preallocated buffer, the gathered
 PCM's parity) is exercised here as 2 ranks sharing cuda:0 over gloo, with
-the collectives staged through host memory.  torch.distributed.run starts
-the ranks as fresh processes; nothing in this test touches the GPU itself.
+the collectives staged through host memory, and as ONE rank over RCCL (a
+one-GPU box cannot hold two RCCL ranks: the process group, the barriers, the
+device max over ranks and the gather's size exchange run through RCCL; the
+point-to-point sends need a second GPU).  torch.distributed.run starts the
+ranks as fresh processes; nothing in this test touches the GPU itself.
 """
 import json
 import os
@@ -46,3 +49,21 @@ def test_bench_two_ranks_gloo(config):
     # rank 0's own timed output against the oracle
     assert d["max_dpcm_lsb"] <= 1 and d["modes"]["fast"]["parity_granules"] > 0
     assert "cpu_baseline" not in d  # an N = 1 figure
+
+
+def test_bench_one_rank_rccl():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(REPO, "bench.py"), "--gpus", "1", "--steps", "2", "--warmup", "1",
+           "--config", "c2", "--backend", "nccl", "--single-mode", "--no-bitstream", "--no-polyphase",
+           "--cpu-repeats", "1"]
+    env = dict(os.environ, OMP_NUM_THREADS="4")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=REPO, env=env)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert r.returncode == 0 and len(lines) == 1, r.stdout[-3000:] + r.stderr[-5000:]
+    d = json.loads(lines[0])
+    print({k: d[k] for k in ("value", "ms_per_step", "n_gpus", "gather_ms", "max_dpcm_lsb")})
+    assert d["n_gpus"] == 1 and d["value"] > 0
+    assert d["gather"]["backend"].startswith("RCCL") and d["gather"]["bytes"] == 20000 * 2304
+    assert d["gather"]["parity"]["max_dpcm_lsb"] <= 1
+    assert d["max_dpcm_lsb"] <= 1
