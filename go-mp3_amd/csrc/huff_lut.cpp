@@ -19,6 +19,7 @@ struct Builder {
   HuffLut* t;
   uint32_t n = 0;
   bool ok = true;
+  uint32_t tree_base = 0;  // the current tree's root block (links count from it)
 
   // Block for the codes `cs`, which share their first `depth` bits; returns
   // the block's offset and its width in *w_out.
@@ -49,11 +50,12 @@ struct Builder {
       int cw = 0;
       const uint32_t child = block(sub[i], depth + w, 6, &cw);
       if (!ok) return 0;
-      if ((child & 1u) || (child >> 1) > 0xfffu) {
+      const uint32_t rel = child - tree_base;
+      if ((rel & 1u) || (rel >> 1) > 0xfffu) {
         ok = false;
         return 0;
       }
-      t->e[off + i] = (uint16_t)(0x8000u | ((uint32_t)cw << 12) | (child >> 1));
+      t->e[off + i] = (uint16_t)(0x8000u | ((uint32_t)cw << 12) | (rel >> 1));
     }
     return off;
   }
@@ -79,7 +81,8 @@ bool build_huff_lut(HuffLut* t) {
       }
     if (cs.empty()) continue;
     int w0 = 0;
-    const uint32_t off = b.block(cs, 0, 8, &w0);
+    b.tree_base = b.n;
+    const uint32_t off = b.block(cs, 0, kHuffRootBits, &w0);
     if (!b.ok) return false;
     tree_root[tree] = off | ((uint32_t)w0 << 24);  // w0 >= 1: never 0
     have[tree] = true;

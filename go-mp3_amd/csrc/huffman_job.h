@@ -114,10 +114,11 @@ struct Reader {
 // *len = its codeword length.
 MP3G_HD_INLINE uint32_t lut_leaf(const uint16_t* T, uint32_t root, uint32_t p, uint32_t* len) {
   int used = (int)(root >> 24);
-  uint32_t e = T[(root & 0xffffffu) + (p >> (32 - used))];
+  const uint32_t base = root & 0xffffffu;
+  uint32_t e = T[base + (p >> (32 - used))];
   while (e & 0x8000u) {
     const int wd = (int)((e >> 12) & 7u);
-    e = T[((e & 0xfffu) << 1) + ((p << used) >> (32 - wd))];
+    e = T[base + ((e & 0xfffu) << 1) + ((p << used) >> (32 - wd))];
     used += wd;
   }
   *len = (e >> 8) & 31u;

@@ -80,8 +80,10 @@ def _masked(g):
 def hjob_host(tmp_path_factory):
     """tests/native/hjob_host.hip: the device job decoder built for the CPU."""
     out = tmp_path_factory.mktemp("native") / "libhjob_host.so"
+    # MP3G_HJOB_FLAGS: extra -D knobs of a variant build (e.g. -DMP3G_HUFF_ROOT_BITS=10)
+    extra = os.environ.get("MP3G_HJOB_FLAGS", "").split()
     subprocess.check_call(["/opt/rocm/bin/hipcc", "-O2", "-std=c++17", "-fPIC", "-shared", "--offload-arch=gfx950",
-                           "-o", str(out), os.path.join(REPO, "tests", "native", "hjob_host.hip"),
+                           *extra, "-o", str(out), os.path.join(REPO, "tests", "native", "hjob_host.hip"),
                            os.path.join(REPO, "go-mp3_amd", "csrc", "huff_lut.cpp")])
     L = C.CDLL(str(out))
     L.hjob_decode_host.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p]
