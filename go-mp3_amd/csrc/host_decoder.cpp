@@ -532,7 +532,9 @@ struct mp3g_decoder {
       if (e == hipSuccess) e = hipMemcpyAsync(d_jobs, si, b_jobs, hipMemcpyHostToDevice, stream);
       if (e == hipSuccess) {
         rc = mp3g_huffman_execute_ex(device, d_jobs, n, d_md, d_gran, d_coef,
-                                     mode_reads_to_count1(mode) ? MP3G_HUFF_ROWS_COUNT1 : 0u, stream);
+                                     (mode_reads_to_count1(mode) ? MP3G_HUFF_ROWS_COUNT1 : 0u) |
+                                         mp3g_huffman_stage_flags(b.jobs.data(), n),
+                                     stream);
         if (rc) return rc;
       }
     } else if (e == hipSuccess) {

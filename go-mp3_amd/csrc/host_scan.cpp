@@ -408,7 +408,10 @@ int mp3g_decode_streams(int device, uint32_t n_streams, const uint8_t* const* da
   rc = e == hipSuccess ? MP3G_OK : abi_fail(MP3G_ERR_DEVICE, "decode_streams: device buffers / H2D");
   if (rc == MP3G_OK)
     rc = mp3g_huffman_execute_ex(device, (const mp3g_hjob*)dj, n, (const uint8_t*)dm, (mp3g_granule*)dg,
-                                 (int16_t*)dc, mode_reads_to_count1(mode) ? MP3G_HUFF_ROWS_COUNT1 : 0u, st);
+                                 (int16_t*)dc,
+                                 (mode_reads_to_count1(mode) ? MP3G_HUFF_ROWS_COUNT1 : 0u) |
+                                     mp3g_huffman_stage_flags(s->jobs.data(), n),
+                                 st);
   if (rc == MP3G_OK)
     rc = mp3g_plan_execute(plan, (const mp3g_granule*)dg, (const int16_t*)dc, nullptr, nullptr, (int16_t*)dp, st);
   if (rc == MP3G_OK) {
@@ -592,7 +595,9 @@ int mp3g_decode_streams_into(int device, uint32_t n_streams, const uint8_t* cons
       rc = mp3g_huffman_execute_ex(device, static_cast<const mp3g_hjob*>(d_jobs[slot].p), ng,
                                 static_cast<const uint8_t*>(d_md[slot].p), static_cast<mp3g_granule*>(d_gran[slot].p),
                                 static_cast<int16_t*>(d_coef[slot].p),
-                                mode_reads_to_count1(mode) ? MP3G_HUFF_ROWS_COUNT1 : 0u, st);
+                                (mode_reads_to_count1(mode) ? MP3G_HUFF_ROWS_COUNT1 : 0u) |
+                                    mp3g_huffman_stage_flags(jobs, ng),
+                                st);
       if (rc == MP3G_OK)
         rc = mp3g_plan_execute(plans[gi], static_cast<const mp3g_granule*>(d_gran[slot].p),
                                static_cast<const int16_t*>(d_coef[slot].p), nullptr, nullptr,

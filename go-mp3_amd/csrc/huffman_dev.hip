@@ -52,22 +52,28 @@ __device__ __forceinline__ uint64_t wave_max(uint64_t v) {
 // 512-thread blocks (better sort, shared tables) were 3 % faster at c3 and
 // 6 % slower at c2.
 #ifndef MP3G_HUFF_BLOCK_STAGE_WORDS
-#define MP3G_HUFF_BLOCK_STAGE_WORDS 3584  // 28 KB: 256 jobs span ~25 KB at 128 kbps
+#define MP3G_HUFF_BLOCK_STAGE_WORDS kHuffStageWords  // 28 KB: 256 jobs span ~25 KB at 128 kbps
 #endif
 constexpr int kBlockStage = MP3G_HUFF_BLOCK_STAGE_WORDS;
+// the wide instantiation (MP3G_HUFF_STAGE_WIDE): 68 KB of stage, 2 blocks per
+// CU.  c3 shape at 320 kbps (no block fits 28 KB): 5.19 ms reading global
+// memory at 16 waves per CU, 4.41 ms staged at 8; at 128 kbps the default
+// is 2.32 ms and the wide one 3.46 ms (tools/huff_time.py c3 / c3hi).
+constexpr int kBlockStageWide = kHuffStageWordsWide;
 constexpr int kBins = 128;  // bin 0: jobs that read nothing; 1 + big_values / 4 <= 73
 
 #ifndef MP3G_HUFF_MAXVGPR
 #define MP3G_HUFF_MAXVGPR 128  // unbounded, the compiler takes 129 (3 waves per SIMD)
 #endif
 #define MP3G_HUFF_SORTED_ATTR __attribute__((amdgpu_num_vgpr(MP3G_HUFF_MAXVGPR)))
+template <int kStage>
 __global__ void __launch_bounds__(kThreads) MP3G_HUFF_SORTED_ATTR
 huffman_sorted_kernel(const mp3g_hjob* __restrict__ jobs, uint64_t n_jobs, const uint8_t* __restrict__ md,
                       mp3g_granule* __restrict__ gran, int16_t* __restrict__ coef, uint32_t full_rows) {
   static_assert(kThreads <= 1024 && kThreads % 64 == 0, "block shape");
   __shared__ uint32_t T2[kHuffMaxEntries / 2];
   __shared__ uint32_t s_root[34], s_lin[34];
-  __shared__ uint64_t stage[kBlockStage + 4];  // + 4: the LDS reader's look-ahead
+  __shared__ uint64_t stage[kStage + 4];  // + 4: the LDS reader's look-ahead
   __shared__ uint32_t s_bin[kBins];
   __shared__ uint16_t s_order[kThreads];
   __shared__ uint64_t s_lo[kWaves], s_hi[kWaves];
@@ -119,7 +125,7 @@ huffman_sorted_kernel(const mp3g_hjob* __restrict__ jobs, uint64_t n_jobs, const
     s_bin[2 * t + 1] = ex + a;
   }
   const uint64_t nwords = hi > lo && lo != ~0ull ? ((hi - lo + 63) >> 6) : 0ull;
-  const bool staged = nwords <= (uint64_t)kBlockStage;  // block-uniform
+  const bool staged = nwords <= (uint64_t)kStage;  // block-uniform
   if (staged) {
     const uint64_t* src = reinterpret_cast<const uint64_t*>(md + (lo >> 3));
     for (uint32_t k = t; k < (uint32_t)nwords; k += kThreads) stage[k] = bswap64(src[k]);
@@ -162,12 +168,15 @@ huffman_sorted_kernel(const mp3g_hjob* __restrict__ jobs, uint64_t n_jobs, const
 }  // namespace huff
 
 hipError_t launch_huffman(const mp3g_hjob* d_jobs, uint64_t n_jobs, const uint8_t* d_md, mp3g_granule* d_gran,
-                          int16_t* d_coef, bool full_rows, hipStream_t stream) {
+                          int16_t* d_coef, bool full_rows, bool wide_stage, hipStream_t stream) {
   if (n_jobs == 0) return hipSuccess;
   const uint64_t blocks = (n_jobs + huff::kThreads - 1) / huff::kThreads;
-  hipLaunchKernelGGL(huff::huffman_sorted_kernel, dim3((uint32_t)blocks),
-                     dim3(huff::kThreads), 0, stream, d_jobs, n_jobs, d_md, d_gran, d_coef,
-                     full_rows ? 1u : 0u);
+  if (wide_stage)
+    hipLaunchKernelGGL(huff::huffman_sorted_kernel<huff::kBlockStageWide>, dim3((uint32_t)blocks),
+                       dim3(huff::kThreads), 0, stream, d_jobs, n_jobs, d_md, d_gran, d_coef, full_rows ? 1u : 0u);
+  else
+    hipLaunchKernelGGL(huff::huffman_sorted_kernel<huff::kBlockStage>, dim3((uint32_t)blocks),
+                       dim3(huff::kThreads), 0, stream, d_jobs, n_jobs, d_md, d_gran, d_coef, full_rows ? 1u : 0u);
   return hipGetLastError();
 }
 

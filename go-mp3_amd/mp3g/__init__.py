@@ -16,7 +16,8 @@ import numpy as np
 __all__ = ["CHANNEL_DTYPE", "GRANULE_DTYPE", "STREAM_DTYPE", "STATE_DTYPE", "MODE_EXACT",
            "MODE_FAST", "FLAG_CHECKED", "FLAG_KERNEL_V1", "FLAG_KERNEL_V2", "FLAG_HOST_HUFFMAN", "STATE_IN", "STATE_OUT", "Mp3gError", "lib", "lib_path",
            "decode_host", "validate", "Plan", "device_count", "streams_for", "parse_stream",
-           "parse_streams", "Decoder", "HJOB_DTYPE", "scan_streams", "huffman_execute", "HUFF_ROWS_COUNT1", "decode_streams"]
+           "parse_streams", "Decoder", "HJOB_DTYPE", "scan_streams", "huffman_execute", "HUFF_ROWS_COUNT1",
+           "HUFF_STAGE_WIDE", "huffman_stage_flags", "decode_streams"]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 
@@ -112,6 +113,8 @@ def lib():
         L.mp3g_lame_toc_offset.restype = C.c_int
         L.mp3g_huffman_execute.argtypes = [C.c_int, vp, u64, vp, vp, vp, vp]
         L.mp3g_huffman_execute_ex.argtypes = [C.c_int, vp, u64, vp, vp, vp, u32, vp]
+        L.mp3g_huffman_stage_flags.argtypes = [vp, u64]
+        L.mp3g_huffman_stage_flags.restype = u32
         L.mp3g_decode_streams.argtypes = [C.c_int, u32, vp, vp, C.c_int, u32, C.POINTER(vp), C.POINTER(u64),
                                           vp, vp]
         L.mp3g_decode_streams_into.argtypes = [C.c_int, u32, vp, vp, C.c_int, u32, u32, vp, u64, C.POINTER(u64),
@@ -270,6 +273,7 @@ def scan_streams(datas, n_threads=0):
 
 
 HUFF_ROWS_COUNT1 = 1  # mp3g_huffman_execute_ex: rows written only up to count1 (+ padding)
+HUFF_STAGE_WIDE = 2  # mp3g_huffman_execute_ex: 68 KB main-data stage per block (high bitrates)
 # fast mode's magnitude bounds (granule_fast.hip kHotS / kHotL1, checked by
 # tests/test_abi_cpu.py): a granule with max |S| > FAST_HOT_S and a time slot
 # whose sum of |S| over the 32 subbands exceeds FAST_HOT_L1 runs in the
@@ -291,6 +295,15 @@ def huffman_execute(d_jobs, n_granules, d_main_data, d_granules, d_coeffs, strea
     else:
         _check(lib().mp3g_huffman_execute(device, p(d_jobs), n_granules, p(d_main_data), p(d_granules),
                                           p(d_coeffs), st))
+
+
+def huffman_stage_flags(jobs, n_granules=None):
+    """mp3g_huffman_stage_flags: HUFF_STAGE_WIDE when most of the batch's
+    256-job blocks fit only the wide main-data stage, else 0 (jobs: the scan's
+    HJOB_DTYPE array, host memory)."""
+    jobs = np.ascontiguousarray(jobs, dtype=HJOB_DTYPE)
+    n = len(jobs) // 2 if n_granules is None else int(n_granules)
+    return int(lib().mp3g_huffman_stage_flags(jobs.ctypes.data, n))
 
 
 class _LameInfo(C.Structure):

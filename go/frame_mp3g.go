@@ -32,7 +32,7 @@ import (
 )
 
 // ABIVersion is the C-ABI version this shim was written against.
-const ABIVersion = 3
+const ABIVersion = 4
 
 // Batch collects parsed frames; DecodeBatch replaces calling Decode() on each.
 // Not safe for concurrent use (like Decoder, decode.go:31-33).

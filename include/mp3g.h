@@ -35,7 +35,7 @@ extern "C" {
  *    fallback (no signature change).
  * 3: streaming input -- mp3g_reader + mp3g_decoder_new_reader, MP3G_ERR_READ;
  *    MP3G_FLAG_KERNEL_V1 retired. */
-#define MP3G_ABI_VERSION 3
+#define MP3G_ABI_VERSION 4
 
 /* ---- status codes ------------------------------------------------------ */
 typedef enum mp3g_status {
@@ -294,8 +294,18 @@ int mp3g_huffman_execute(int device, const mp3g_hjob* d_jobs, uint64_t n_granule
  * are zero (maindata/huffman.go:127-134).  The batch and decoder APIs use it
  * for those modes (c3 main-data kernel -13 %). */
 #define MP3G_HUFF_ROWS_COUNT1 1u
+/* MP3G_HUFF_STAGE_WIDE (ABI 4): each 256-job block stages up to 68 KB of its
+ * main data in LDS (8 waves per CU) instead of 28 KB (16 waves per CU).
+ * Blocks whose main data does not fit the stage read it from global memory,
+ * which is slower: above ~140 kbps no block of 256 jobs fits 28 KB.
+ * mp3g_huffman_stage_flags tells which suits a batch. */
+#define MP3G_HUFF_STAGE_WIDE 2u
 int mp3g_huffman_execute_ex(int device, const mp3g_hjob* d_jobs, uint64_t n_granules, const uint8_t* d_main_data,
                             mp3g_granule* d_granules, int16_t* d_coeffs, uint32_t flags, void* hip_stream);
+/* Host-side advice for mp3g_huffman_execute_ex: MP3G_HUFF_STAGE_WIDE when
+ * more of the batch's 256-job blocks fit only the wide stage than fit the
+ * default one, else 0.  `jobs`: the scan's jobs (host memory, 2 * n_granules). */
+uint32_t mp3g_huffman_stage_flags(const mp3g_hjob* jobs, uint64_t n_granules);
 
 /* Bitstreams in, PCM out (the batch drop-in): scan on the host, Huffman + DSP
  * on `device`.  *pcm (library-allocated, free with mp3g_free) holds

@@ -28,7 +28,7 @@ from test_scan_cpu import WRITER_CASES
 pytestmark = pytest.mark.gpu
 
 
-def gpu_parse(gpu, datas):
+def gpu_parse(gpu, datas, flags=0):
     """scan on the host, Huffman on cuda:0 -> (granules, coeffs, streams, end_status)."""
     import torch
     dev = torch.device("cuda:0")
@@ -40,15 +40,15 @@ def gpu_parse(gpu, datas):
     d_j = torch.from_numpy(s["jobs"].view(np.uint8).copy()).to(dev)
     d_m = torch.from_numpy(s["main_data"].copy()).to(dev)
     d_c = torch.full((n * 1152,), 0x5A5A, dtype=torch.int16, device=dev)  # poison: every line must be written
-    gpu.huffman_execute(d_j, n, d_m, d_g, d_c, stream=torch.cuda.current_stream(dev).cuda_stream)
+    gpu.huffman_execute(d_j, n, d_m, d_g, d_c, stream=torch.cuda.current_stream(dev).cuda_stream, flags=flags)
     torch.cuda.synchronize(dev)
     g = d_g.cpu().numpy().view(gpu.GRANULE_DTYPE)
     c = d_c.cpu().numpy().reshape(n, 2, 576)
     return g, c, s["streams"], s["end_status"]
 
 
-def assert_same_as_host(gpu, datas, what):
-    g, c, s, st = gpu_parse(gpu, datas)
+def assert_same_as_host(gpu, datas, what, flags=0):
+    g, c, s, st = gpu_parse(gpu, datas, flags)
     g2, c2, s2, st2 = gpu.parse_streams(datas, n_threads=4)
     assert np.array_equal(st, st2), (what, st, st2)
     assert np.array_equal(s, s2), what
@@ -195,3 +195,16 @@ def test_rows_to_count1(gpu, sample_files):
     assert (c1 == 0x5A5A).any(), "the tails should be left unwritten"
     for mode in p0:
         assert np.array_equal(p0[mode], p1[mode]), mode
+
+
+@pytest.mark.parametrize("bitrate_index", [9, 11, 14])
+@pytest.mark.parametrize("stage", ["default", "wide"])
+def test_stage_sizes_at_bitrates(gpu, bitrate_index, stage):
+    """Both main-data stages (MP3G_HUFF_STAGE_WIDE) at 128, 192 and 320 kbps:
+    staged blocks and blocks read from global memory give the host parse's
+    descriptors and coefficients byte for byte (64 streams x 48 frames, 384
+    blocks of 256 jobs)."""
+    from mp3g import synth
+    datas = [synth.encode_stream(7000 + k, 48, bitrate_index=bitrate_index) for k in range(64)]
+    flags = gpu.HUFF_STAGE_WIDE if stage == "wide" else 0
+    assert_same_as_host(gpu, datas, f"bitrate index {bitrate_index}, {stage} stage", flags)

@@ -178,3 +178,15 @@ def test_scan_direct_and_fallback_paths_agree(sample_files):
     assert a["jobs"].tobytes() == b["jobs"][:2 * n].tobytes()
     md_end = (int(a["jobs"]["bit_end"].max()) + 7) // 8
     assert a["main_data"][:md_end].tobytes() == b["main_data"][:md_end].tobytes()
+
+
+def test_huffman_stage_advice():
+    """mp3g_huffman_stage_flags (host): the default 28 KB main-data stage holds a
+    256-job block at 128 kbps, only the wide one at 320 kbps."""
+    import mp3g
+    from mp3g import synth
+    for br, want in ((9, 0), (14, mp3g.HUFF_STAGE_WIDE)):
+        datas = [synth.encode_stream(1 + k, 256, bitrate_index=br) for k in range(8)]
+        s = mp3g.scan_streams(datas, n_threads=4)
+        assert mp3g.huffman_stage_flags(s["jobs"]) == want, br
+    assert mp3g.huffman_stage_flags(np.zeros(0, mp3g.HJOB_DTYPE)) == 0
