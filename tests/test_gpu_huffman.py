@@ -16,6 +16,7 @@ oracle's PCM: bit-exact in exact mode, +-1 LSB in fast mode.
 """
 import hashlib
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -208,3 +209,30 @@ def test_stage_sizes_at_bitrates(gpu, bitrate_index, stage):
     datas = [synth.encode_stream(7000 + k, 48, bitrate_index=bitrate_index) for k in range(64)]
     flags = gpu.HUFF_STAGE_WIDE if stage == "wide" else 0
     assert_same_as_host(gpu, datas, f"bitrate index {bitrate_index}, {stage} stage", flags)
+
+
+def test_random_writer_configs_vs_oracle(gpu):
+    """A short run of tools/soak.py's random configurations (MPEG-1 / LSF, every
+    channel mode, bitrate and sample rate, MS / IS / mixed / short rates):
+    the batch drop-in's exact PCM is the oracle's byte for byte, fast within
+    1 LSB (the tool itself ran 85,884 such streams, profiles/r04_soak.json)."""
+    sys.path.insert(0, os.path.join(os.path.dirname(GOLDEN), "..", "tools"))
+    from soak import stream_params
+    from mp3g import synth
+    rng = np.random.default_rng(20261018)
+    datas = []
+    while len(datas) < 64:
+        try:
+            datas.append(synth.encode_stream(int(rng.integers(1, 2**31)), int(rng.integers(1, 64)),
+                                             **stream_params(rng)))
+        except RuntimeError:  # a configuration the writer cannot fill
+            continue
+    pcm, streams, st = gpu.decode_streams(datas, mode=gpu.MODE_EXACT)
+    pcm_f, streams_f, _ = gpu.decode_streams(datas, mode=gpu.MODE_FAST)
+    for k, d in enumerate(datas):
+        ost, opcm = oracle.decode_all(d)
+        lo, m = int(streams[k]["first_granule"]), int(streams[k]["n_granules"])
+        assert ost == oracle.ORC_OK and st[k] == 7, k
+        assert pcm[lo:lo + m].tobytes() == opcm, k
+        f = pcm_f[int(streams_f[k]["first_granule"]):][:m].astype(np.int32)
+        assert np.abs(f - pcm[lo:lo + m]).max(initial=0) <= 1, k
