@@ -910,6 +910,9 @@ int mp3g_decoder_seek(mp3g_decoder* d, int64_t offset, int whence, int64_t* newp
   if ((int)d->frame_ends.size() < need) {  // the reference's 2nd readFrame failed
     rc = d->pending;
     d->pending = MP3G_OK;
+    // its source now stands after the failed frame (where the scan stopped): a
+    // later seek that reads nothing must not rewind it to the frame before
+    d->frame_src_ends.clear();
     return rc;
   }
   const size_t ref_len = d->frame_ends[need - 1];  // the reference's d.buf holds exactly `need` frames here

@@ -1442,14 +1442,20 @@ int orc_decoder_seek(orc_decoder* d, int64_t offset, int whence, int64_t* newpos
     st = dec_read_frame(d);
     if (st) return st;
     d->buf_off = (long)(d->bytes_per_frame + d->pos % d->bytes_per_frame);
-    if (d->buf_off > d->buf_len) return ORC_ERR_PANIC;
+    if (d->buf_off > d->buf_len) { /* slice bounds out of range in the reference */
+      dec_buf_reset(d); /* (the process would have ended: leave no negative span for a later Read) */
+      return ORC_ERR_PANIC;
+    }
   } else {
     if (d->n_starts == 0) return ORC_ERR_PANIC;
     if (src_seek(&d->src, d->frame_starts[0], 0, NULL)) return ORC_ERR;
     int st = dec_read_frame(d);
     if (st) return st;
     d->buf_off = (long)d->pos;
-    if (d->buf_off > d->buf_len) return ORC_ERR_PANIC;
+    if (d->buf_off > d->buf_len) {
+      dec_buf_reset(d);
+      return ORC_ERR_PANIC;
+    }
   }
   dec_buf_compact(d);
   *newpos = npos;

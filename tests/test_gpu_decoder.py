@@ -248,3 +248,36 @@ def test_read_full_spans_then_seek(gpu, sample_files, name):
         st2, want = _oracle_read_full(o, cap)
         assert st == ST[st2] and buf[:k].tobytes() == want, f"step {step}"
         assert d.seek(off, whence) == o.seek(off, whence), f"step {step} seek"
+
+
+def test_failed_seek_then_seek_to_end_then_read(gpu):
+    """A seek whose second readFrame fails (decode.go:128-133) leaves the
+    reference's source after the failed frame; a later seek to the end reads
+    nothing (decode.go:110-113), so the next Read decodes the frame after the
+    failed one from there -- not the failed frame again.  The input is a
+    corrupted stream of the Layer III writer (tools/soak.py, seed 4 round 5)."""
+    import os
+    data = open(os.path.join(os.path.dirname(__file__), "golden", "soak", "failed_seek_then_end.mp3"), "rb").read()
+    d, o = both(gpu, data)
+    for n in (4608, 300000):
+        st, b = d.read(n)
+        st2, b2 = o.read(n)
+        assert st == ST[st2] and b == b2
+    assert d.seek_to_time_ns(2311823882) == ST[o.seek_to_time_ns(2311823882)]
+    assert d.seek_to_sample(30562) == ST[o.seek_to_sample(30562)]
+    for n in (20000, 4096, 3, 3):
+        st, b = d.read(n)
+        st2, b2 = o.read(n)
+        assert st == ST[st2] and b == b2
+    r, r2 = d.seek_to_sample(7981), o.seek_to_sample(7981)
+    assert r2 == oracle.ORC_ERR and r == ST[r2]  # the warm-up's second frame is corrupt
+    st, b = d.read(3)
+    st2, b2 = o.read(3)
+    assert st == ST[st2] and b == b2
+    assert d.seek_to_time_ns(1689226975) == ST[o.seek_to_time_ns(1689226975)]
+    assert d.pos == o.pos == o.length
+    for n in (100, 4608, 300000):
+        st, b = d.read(n)
+        st2, b2 = o.read(n)
+        assert st == ST[st2] and b == b2, (n, st, st2, len(b), len(b2))
+        assert d.pos == o.pos
