@@ -67,23 +67,51 @@ def mutate(data, rng):
     return bytes(b)
 
 
+class PieceReader:
+    """io.Reader (+ io.Seeker) over bytes, 1..4096 bytes per Read (the
+    streaming input of mp3g_decoder_new_reader)."""
+
+    def __init__(self, data, seed):
+        self.data, self.off, self.rng = data, 0, np.random.default_rng(seed)
+
+    def read(self, n):
+        k = min(n, int(self.rng.integers(1, 4097)), len(self.data) - self.off)
+        b = self.data[self.off:self.off + max(k, 0)]
+        self.off += len(b)
+        return b
+
+    def seek(self, off, whence):
+        a = off if whence == 0 else self.off + off if whence == 1 else len(self.data) + off
+        if a < 0:
+            raise ValueError("negative position")
+        self.off = a
+        return a
+
+
 def decoder_ops(mp3g, oracle, data, rng, n_ops, mode, log):
     """A random Read / Seek / time-API sequence on the product's decoder
     (mp3g_decoder_*, the io.Reader drop-in) and the oracle's; returns the
     first divergence or None (exact mode: same bytes; fast: within 1 LSB)."""
     st_map = {oracle.ORC_OK: 0, oracle.ORC_EOF: 7, oracle.ORC_ERR: 6, oracle.ORC_ERR_PANIC: 8}
     seekable = bool(rng.random() < 0.8)
+    streaming = bool(rng.random() < 0.5)  # through reader callbacks, 1..4096-byte pieces
+
+    def new_product():
+        if streaming:
+            r = PieceReader(data, int(rng.integers(1, 2**31)))
+            return mp3g.Decoder.from_reader(r.read, r.seek if seekable else None, mode=mode)
+        return mp3g.Decoder(data, seekable=seekable, mode=mode)
     try:
         o = oracle.Decoder(data, seekable=seekable)
     except IOError:  # NewDecoder fails (no frame): the product's must fail too
         try:
-            mp3g.Decoder(data, seekable=seekable, mode=mode)
+            new_product()
         except mp3g.Mp3gError:
             return None
         return ("new decoder succeeded where the oracle's failed",)
-    d = mp3g.Decoder(data, seekable=seekable, mode=mode)
+    d = new_product()
     L = max(o.length, 1)
-    log.append(("new", seekable, mode))
+    log.append(("new", seekable, mode, streaming))
     for step in range(n_ops):
         op = int(rng.integers(0, 6 if seekable else 3))
         if op < 3:

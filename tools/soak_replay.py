@@ -18,7 +18,9 @@ def main():
     data = open(base + ".mp3", "rb").read()
     meta = json.load(open(base + ".json"))
     ops = meta["ops"]
-    _, seekable, mode = ops[0]
+    _, seekable, mode = ops[0][:3]
+    if len(ops[0]) > 3 and ops[0][3]:
+        print("(recorded on the streaming reader; replayed in memory)")
     o = oracle.Decoder(data, seekable=seekable)
     d = mp3g.Decoder(data, seekable=seekable, mode=mode)
     print(f"len {len(data)} seekable {seekable} mode {mode} length {d.length} / {o.length} "
