@@ -262,7 +262,8 @@ def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle, pip
            # the coefficient lines below count1 (MP3G_HUFF_ROWS_COUNT1; full rows
            # would be 2 x 1152 B) + 2 x 63 B scale factors / count1 out per granule
            "huffman_rows": "to count1 (mp3g_huffman_execute_ex, MP3G_HUFF_ROWS_COUNT1)",
-           "huffman_stage": "wide (68 KB)" if hflags & mp3g.HUFF_STAGE_WIDE else "default (28 KB)",
+           "huffman_stage": "wide (68 KB)" if hflags & mp3g.HUFF_STAGE_WIDE else
+                            "mid (42 KB)" if hflags & mp3g.HUFF_STAGE_MID else "default (28 KB)",
            "huffman_coef_bytes_written": coef_bytes,
            "huffman_algorithmic_bytes_per_launch": md + n * (96 + 126) + coef_bytes,
            "huffman_algorithmic_gbps": round((md + n * (96 + 126) + coef_bytes) / (huff_ms * 1e-3) / 1e9, 2),

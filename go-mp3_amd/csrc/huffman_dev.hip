@@ -55,10 +55,13 @@ __device__ __forceinline__ uint64_t wave_max(uint64_t v) {
 #define MP3G_HUFF_BLOCK_STAGE_WORDS kHuffStageWords  // 28 KB: 256 jobs span ~25 KB at 128 kbps
 #endif
 constexpr int kBlockStage = MP3G_HUFF_BLOCK_STAGE_WORDS;
-// the wide instantiation (MP3G_HUFF_STAGE_WIDE): 68 KB of stage, 2 blocks per
-// CU.  c3 shape at 320 kbps (no block fits 28 KB): 5.19 ms reading global
-// memory at 16 waves per CU, 4.41 ms staged at 8; at 128 kbps the default
-// is 2.32 ms and the wide one 3.46 ms (tools/huff_time.py c3 / c3hi).
+// the larger instantiations for higher bitrates (tools/huff_time.py, c3's
+// shape): MP3G_HUFF_STAGE_MID, 42 KB of stage, 3 blocks per CU -- at 192 kbps
+// (no block fits 28 KB) 2.97 ms against 4.58 ms reading global memory at 16
+// waves per CU and 3.84 ms with the wide stage; MP3G_HUFF_STAGE_WIDE, 68 KB, 2
+// blocks per CU -- at 320 kbps 4.41 ms against 5.19 ms reading global memory.
+// At 128 kbps the default is 2.18-2.32 ms, the mid one 2.54, the wide 3.46.
+constexpr int kBlockStageMid = kHuffStageWordsMid;
 constexpr int kBlockStageWide = kHuffStageWordsWide;
 constexpr int kBins = 128;  // bin 0: jobs that read nothing; 1 + big_values / 4 <= 73
 
@@ -168,11 +171,14 @@ huffman_sorted_kernel(const mp3g_hjob* __restrict__ jobs, uint64_t n_jobs, const
 }  // namespace huff
 
 hipError_t launch_huffman(const mp3g_hjob* d_jobs, uint64_t n_jobs, const uint8_t* d_md, mp3g_granule* d_gran,
-                          int16_t* d_coef, bool full_rows, bool wide_stage, hipStream_t stream) {
+                          int16_t* d_coef, bool full_rows, int stage, hipStream_t stream) {
   if (n_jobs == 0) return hipSuccess;
   const uint64_t blocks = (n_jobs + huff::kThreads - 1) / huff::kThreads;
-  if (wide_stage)
+  if (stage == 2)
     hipLaunchKernelGGL(huff::huffman_sorted_kernel<huff::kBlockStageWide>, dim3((uint32_t)blocks),
+                       dim3(huff::kThreads), 0, stream, d_jobs, n_jobs, d_md, d_gran, d_coef, full_rows ? 1u : 0u);
+  else if (stage == 1)
+    hipLaunchKernelGGL(huff::huffman_sorted_kernel<huff::kBlockStageMid>, dim3((uint32_t)blocks),
                        dim3(huff::kThreads), 0, stream, d_jobs, n_jobs, d_md, d_gran, d_coef, full_rows ? 1u : 0u);
   else
     hipLaunchKernelGGL(huff::huffman_sorted_kernel<huff::kBlockStage>, dim3((uint32_t)blocks),

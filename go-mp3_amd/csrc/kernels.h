@@ -47,13 +47,15 @@ int chunks_per_cu(int variant);
 // Main-data decode (huffman_dev.hip): one lane per (granule, channel) job.
 // full_rows = false: rows written only up to count1 (+ padding), enough for
 // the one-wave plan kernels (fast v3, exact v4) -- MP3G_HUFF_ROWS_COUNT1.
-// wide_stage: the 68 KB-stage instantiation (MP3G_HUFF_STAGE_WIDE).
+// stage: 0 = the default 28 KB instantiation, 1 = 42 KB (MP3G_HUFF_STAGE_MID),
+// 2 = 68 KB (MP3G_HUFF_STAGE_WIDE).
 hipError_t launch_huffman(const mp3g_hjob* d_jobs, uint64_t n_jobs, const uint8_t* d_md, mp3g_granule* d_gran,
-                          int16_t* d_coef, bool full_rows, bool wide_stage, hipStream_t stream);
+                          int16_t* d_coef, bool full_rows, int stage, hipStream_t stream);
 // The main-data kernel's blocks (jobs per block, LDS stage in 64-bit words:
 // default and wide), for the host-side stage advice.
 constexpr int kHuffJobsPerBlock = 256;
 constexpr int kHuffStageWords = 3584;       // 28 KB: 256 jobs span ~25 KB at 128 kbps
+constexpr int kHuffStageWordsMid = 5376;   // 42 KB: ~40 KB at 192 kbps (3 blocks per CU)
 constexpr int kHuffStageWordsWide = 8704;  // 68 KB: ~67 KB at 320 kbps
 
 // Diagnostic: fast kernel with per-phase s_memtime sums (8 per chunk) in d_stamps.

@@ -405,7 +405,8 @@ int mp3g_huffman_execute(int device, const mp3g_hjob* d_jobs, uint64_t n_granule
 
 int mp3g_huffman_execute_ex(int device, const mp3g_hjob* d_jobs, uint64_t n_granules, const uint8_t* d_md,
                             mp3g_granule* d_gran, int16_t* d_coef, uint32_t flags, void* hip_stream) {
-  if (flags & ~(uint32_t)(MP3G_HUFF_ROWS_COUNT1 | MP3G_HUFF_STAGE_WIDE))
+  if (flags & ~(uint32_t)(MP3G_HUFF_ROWS_COUNT1 | MP3G_HUFF_STAGE_WIDE | MP3G_HUFF_STAGE_MID) ||
+      ((flags & MP3G_HUFF_STAGE_WIDE) && (flags & MP3G_HUFF_STAGE_MID)))
     return fail(MP3G_ERR_INVALID_ARGUMENT, "huffman flags");
   if (n_granules == 0) return MP3G_OK;
   if (!d_jobs || !d_md || !d_gran || !d_coef) return fail(MP3G_ERR_INVALID_ARGUMENT, "null device buffer");
@@ -414,7 +415,8 @@ int mp3g_huffman_execute_ex(int device, const mp3g_hjob* d_jobs, uint64_t n_gran
   int st = ensure_device(device);
   if (st) return st;
   HIP_TRY(launch_huffman(d_jobs, 2 * n_granules, d_md, d_gran, d_coef, !(flags & MP3G_HUFF_ROWS_COUNT1),
-                         (flags & MP3G_HUFF_STAGE_WIDE) != 0, static_cast<hipStream_t>(hip_stream)));
+                         (flags & MP3G_HUFF_STAGE_WIDE) ? 2 : (flags & MP3G_HUFF_STAGE_MID) ? 1 : 0,
+                         static_cast<hipStream_t>(hip_stream)));
   return MP3G_OK;
 }
 
@@ -424,7 +426,7 @@ int mp3g_huffman_execute_ex(int device, const mp3g_hjob* d_jobs, uint64_t n_gran
 uint32_t mp3g_huffman_stage_flags(const mp3g_hjob* jobs, uint64_t n_granules) {
   if (!jobs) return 0u;
   const uint64_t n = 2 * n_granules;
-  uint64_t fit = 0, wide_only = 0;
+  uint64_t fit = 0, mid = 0, wide = 0, blocks = 0;  // blocks that fit each stage
   for (uint64_t b0 = 0; b0 < n; b0 += kHuffJobsPerBlock) {
     uint64_t lo = ~0ull, hi = 0;
     for (uint64_t j = b0; j < n && j < b0 + kHuffJobsPerBlock; j++) {
@@ -433,10 +435,15 @@ uint32_t mp3g_huffman_stage_flags(const mp3g_hjob* jobs, uint64_t n_granules) {
       hi = std::max<uint64_t>(hi, jobs[j].bit_end);
     }
     const uint64_t words = hi > lo && lo != ~0ull ? (hi - lo + 63) >> 6 : 0;
-    if (words <= (uint64_t)kHuffStageWords) fit++;
-    else if (words <= (uint64_t)kHuffStageWordsWide) wide_only++;
+    blocks++;
+    fit += words <= (uint64_t)kHuffStageWords;
+    mid += words <= (uint64_t)kHuffStageWordsMid;
+    wide += words <= (uint64_t)kHuffStageWordsWide;
   }
-  return wide_only > fit ? MP3G_HUFF_STAGE_WIDE : 0u;
+  // the smallest stage (the most waves per CU) that holds 90 % of the blocks
+  if (10 * fit >= 9 * blocks) return 0u;
+  if (10 * mid >= 9 * blocks) return MP3G_HUFF_STAGE_MID;
+  return MP3G_HUFF_STAGE_WIDE;
 }
 
 // stamped launch of a fast plan: kFastStampSlots per chunk into h

@@ -17,7 +17,7 @@ __all__ = ["CHANNEL_DTYPE", "GRANULE_DTYPE", "STREAM_DTYPE", "STATE_DTYPE", "MOD
            "MODE_FAST", "FLAG_CHECKED", "FLAG_KERNEL_V1", "FLAG_KERNEL_V2", "FLAG_HOST_HUFFMAN", "STATE_IN", "STATE_OUT", "Mp3gError", "lib", "lib_path",
            "decode_host", "validate", "Plan", "device_count", "streams_for", "parse_stream",
            "parse_streams", "Decoder", "HJOB_DTYPE", "scan_streams", "huffman_execute", "HUFF_ROWS_COUNT1",
-           "HUFF_STAGE_WIDE", "huffman_stage_flags", "decode_streams"]
+           "HUFF_STAGE_WIDE", "HUFF_STAGE_MID", "huffman_stage_flags", "decode_streams"]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 
@@ -273,7 +273,8 @@ def scan_streams(datas, n_threads=0):
 
 
 HUFF_ROWS_COUNT1 = 1  # mp3g_huffman_execute_ex: rows written only up to count1 (+ padding)
-HUFF_STAGE_WIDE = 2  # mp3g_huffman_execute_ex: 68 KB main-data stage per block (high bitrates)
+HUFF_STAGE_WIDE = 2  # mp3g_huffman_execute_ex: 68 KB main-data stage per block (~320 kbps)
+HUFF_STAGE_MID = 4  # mp3g_huffman_execute_ex: 42 KB main-data stage per block (~160-200 kbps)
 # fast mode's magnitude bounds (granule_fast.hip kHotS / kHotL1, checked by
 # tests/test_abi_cpu.py): a granule with max |S| > FAST_HOT_S and a time slot
 # whose sum of |S| over the 32 subbands exceeds FAST_HOT_L1 runs in the
@@ -298,9 +299,9 @@ def huffman_execute(d_jobs, n_granules, d_main_data, d_granules, d_coeffs, strea
 
 
 def huffman_stage_flags(jobs, n_granules=None):
-    """mp3g_huffman_stage_flags: HUFF_STAGE_WIDE when most of the batch's
-    256-job blocks fit only the wide main-data stage, else 0 (jobs: the scan's
-    HJOB_DTYPE array, host memory)."""
+    """mp3g_huffman_stage_flags: the smallest main-data stage (0, HUFF_STAGE_MID,
+    HUFF_STAGE_WIDE) that holds 90 % of the batch's 256-job blocks (jobs: the
+    scan's HJOB_DTYPE array, host memory)."""
     jobs = np.ascontiguousarray(jobs, dtype=HJOB_DTYPE)
     n = len(jobs) // 2 if n_granules is None else int(n_granules)
     return int(lib().mp3g_huffman_stage_flags(jobs.ctypes.data, n))

@@ -294,17 +294,20 @@ int mp3g_huffman_execute(int device, const mp3g_hjob* d_jobs, uint64_t n_granule
  * are zero (maindata/huffman.go:127-134).  The batch and decoder APIs use it
  * for those modes (c3 main-data kernel -13 %). */
 #define MP3G_HUFF_ROWS_COUNT1 1u
-/* MP3G_HUFF_STAGE_WIDE (ABI 4): each 256-job block stages up to 68 KB of its
- * main data in LDS (8 waves per CU) instead of 28 KB (16 waves per CU).
- * Blocks whose main data does not fit the stage read it from global memory,
- * which is slower: above ~140 kbps no block of 256 jobs fits 28 KB.
+/* Main-data stage per 256-job block (ABI 4): by default 28 KB of LDS (16
+ * waves per CU); MP3G_HUFF_STAGE_MID 42 KB (12 waves per CU);
+ * MP3G_HUFF_STAGE_WIDE 68 KB (8 waves per CU).  A block whose main data does
+ * not fit its stage reads it from global memory, which is slower: 256 jobs
+ * span ~25 KB at 128 kbps, ~40 KB at 192, ~67 KB at 320.
  * mp3g_huffman_stage_flags tells which suits a batch. */
 #define MP3G_HUFF_STAGE_WIDE 2u
+#define MP3G_HUFF_STAGE_MID 4u
 int mp3g_huffman_execute_ex(int device, const mp3g_hjob* d_jobs, uint64_t n_granules, const uint8_t* d_main_data,
                             mp3g_granule* d_granules, int16_t* d_coeffs, uint32_t flags, void* hip_stream);
-/* Host-side advice for mp3g_huffman_execute_ex: MP3G_HUFF_STAGE_WIDE when
- * more of the batch's 256-job blocks fit only the wide stage than fit the
- * default one, else 0.  `jobs`: the scan's jobs (host memory, 2 * n_granules). */
+/* Host-side advice for mp3g_huffman_execute_ex: the smallest stage (0,
+ * MP3G_HUFF_STAGE_MID or MP3G_HUFF_STAGE_WIDE) that holds 90 % of the batch's
+ * 256-job blocks, else MP3G_HUFF_STAGE_WIDE.  `jobs`: the scan's jobs (host
+ * memory, 2 * n_granules). */
 uint32_t mp3g_huffman_stage_flags(const mp3g_hjob* jobs, uint64_t n_granules);
 
 /* Bitstreams in, PCM out (the batch drop-in): scan on the host, Huffman + DSP

@@ -199,15 +199,15 @@ def test_rows_to_count1(gpu, sample_files):
 
 
 @pytest.mark.parametrize("bitrate_index", [9, 11, 14])
-@pytest.mark.parametrize("stage", ["default", "wide"])
+@pytest.mark.parametrize("stage", ["default", "mid", "wide"])
 def test_stage_sizes_at_bitrates(gpu, bitrate_index, stage):
-    """Both main-data stages (MP3G_HUFF_STAGE_WIDE) at 128, 192 and 320 kbps:
+    """The three main-data stages (default, MP3G_HUFF_STAGE_MID / _WIDE) at 128, 192 and 320 kbps:
     staged blocks and blocks read from global memory give the host parse's
     descriptors and coefficients byte for byte (64 streams x 48 frames, 384
     blocks of 256 jobs)."""
     from mp3g import synth
     datas = [synth.encode_stream(7000 + k, 48, bitrate_index=bitrate_index) for k in range(64)]
-    flags = gpu.HUFF_STAGE_WIDE if stage == "wide" else 0
+    flags = {"default": 0, "mid": gpu.HUFF_STAGE_MID, "wide": gpu.HUFF_STAGE_WIDE}[stage]
     assert_same_as_host(gpu, datas, f"bitrate index {bitrate_index}, {stage} stage", flags)
 
 

@@ -182,10 +182,10 @@ def test_scan_direct_and_fallback_paths_agree(sample_files):
 
 def test_huffman_stage_advice():
     """mp3g_huffman_stage_flags (host): the default 28 KB main-data stage holds a
-    256-job block at 128 kbps, only the wide one at 320 kbps."""
+    256-job block at 128 kbps, the 42 KB one at 192 kbps, the 68 KB one at 320."""
     import mp3g
     from mp3g import synth
-    for br, want in ((9, 0), (14, mp3g.HUFF_STAGE_WIDE)):
+    for br, want in ((9, 0), (11, mp3g.HUFF_STAGE_MID), (14, mp3g.HUFF_STAGE_WIDE)):
         datas = [synth.encode_stream(1 + k, 256, bitrate_index=br) for k in range(8)]
         s = mp3g.scan_streams(datas, n_threads=4)
         assert mp3g.huffman_stage_flags(s["jobs"]) == want, br

@@ -40,7 +40,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--configs", default="c2,c3")
-    ap.add_argument("--stage", choices=["auto", "default", "wide"], default="auto",
+    ap.add_argument("--stage", choices=["auto", "default", "mid", "wide"], default="auto",
                     help="main-data stage: mp3g_huffman_stage_flags' choice, or forced")
     ap.add_argument("--full-rows", action="store_true", help="write whole rows (default: rows to count1, "
                     "what the plan kernels read)")
@@ -54,7 +54,7 @@ def main():
     for cfg in a.configs.split(","):
         # c3hi: c3's shape at 320 kbps (bitrate index 14): main data ~2.6x c3's
         ns, nf = (1, 10000) if cfg == "c2" else (1024, 1024)
-        br = 14 if cfg == "c3hi" else None
+        br = 14 if cfg == "c3hi" else 11 if cfg == "c3mid" else None  # 320 / 192 kbps
         with ThreadPoolExecutor(16) as ex:
             datas = list(ex.map(lambda k: synth.encode_stream(1 + k, nf, bitrate_index=br), range(ns)))
         s = mp3g.scan_streams(datas, n_threads=16)
@@ -66,10 +66,9 @@ def main():
         d_c = torch.zeros(n * 1152, dtype=torch.int16, device=dev)  # zeros: a checksum of rows to count1
         h = st.cuda_stream
         fl = (0 if a.full_rows else mp3g.HUFF_ROWS_COUNT1) | mp3g.huffman_stage_flags(s["jobs"], n)
-        if a.stage == "default":
-            fl &= ~mp3g.HUFF_STAGE_WIDE
-        elif a.stage == "wide":
-            fl |= mp3g.HUFF_STAGE_WIDE
+        if a.stage != "auto":
+            fl &= ~(mp3g.HUFF_STAGE_WIDE | mp3g.HUFF_STAGE_MID)
+            fl |= {"default": 0, "mid": mp3g.HUFF_STAGE_MID, "wide": mp3g.HUFF_STAGE_WIDE}[a.stage]
         for _ in range(5):
             mp3g.huffman_execute(d_j, n, d_m, d_g, d_c, stream=h, flags=fl)
         torch.cuda.synchronize(dev)
@@ -83,7 +82,8 @@ def main():
         crc = int(d_c.view(torch.int32).sum().item()) & 0xffffffff
         print(f"{os.environ.get('MP3G_LIB', 'default'):>28} {cfg} huffman_ms {ms:.4f} "
               f"frames_per_s {n / 2 / ms * 1e3:.4g} coef_sum {crc:08x} staged_blocks {staged:.3f} "
-              f"stage {'wide' if fl & mp3g.HUFF_STAGE_WIDE else 'default'}", flush=True)
+              f"stage {'wide' if fl & mp3g.HUFF_STAGE_WIDE else 'mid' if fl & mp3g.HUFF_STAGE_MID else 'default'}",
+              flush=True)
         del d_g, d_j, d_m, d_c
         time.sleep(0.1)
 
