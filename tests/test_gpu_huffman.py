@@ -236,3 +236,24 @@ def test_random_writer_configs_vs_oracle(gpu):
         assert pcm[lo:lo + m].tobytes() == opcm, k
         f = pcm_f[int(streams_f[k]["first_granule"]):][:m].astype(np.int32)
         assert np.abs(f - pcm[lo:lo + m]).max(initial=0) <= 1, k
+
+
+@pytest.mark.parametrize("bitrate_index", [11, 14])
+def test_bitstream_path_high_bitrates_vs_oracle(gpu, bitrate_index):
+    """The batch drop-in at 192 / 320 kbps, where it picks the mid / wide
+    main-data stage itself (mp3g_huffman_stage_flags): exact PCM = the
+    oracle's NewDecoder + ReadAll byte for byte, fast within 1 LSB."""
+    from mp3g import synth
+    datas = [synth.encode_stream(500 + k, 96, bitrate_index=bitrate_index, p_event=0.1, p_mixed=0.05)
+             for k in range(32)]
+    s = gpu.scan_streams(datas, n_threads=4)
+    want = gpu.HUFF_STAGE_MID if bitrate_index == 11 else gpu.HUFF_STAGE_WIDE
+    assert gpu.huffman_stage_flags(s["jobs"]) == want
+    pcm, streams, st = gpu.decode_streams(datas, mode=gpu.MODE_EXACT)
+    pcm_f, _, _ = gpu.decode_streams(datas, mode=gpu.MODE_FAST)
+    for k, d in enumerate(datas):
+        ost, opcm = oracle.decode_all(d)
+        lo, m = int(streams[k]["first_granule"]), int(streams[k]["n_granules"])
+        assert ost == oracle.ORC_OK and st[k] == 7
+        assert pcm[lo:lo + m].tobytes() == opcm, k
+    assert np.abs(pcm_f.astype(np.int32) - pcm).max() <= 1
