@@ -422,11 +422,20 @@ int mp3g_huffman_execute_ex(int device, const mp3g_hjob* d_jobs, uint64_t n_gran
 
 // The kernel's blocks are kHuffJobsPerBlock consecutive jobs; a block stages
 // the main data from its lowest job base to its highest bit_end (jobs that
-// read nothing aside) when that span fits the stage (huffman_dev.hip).
+// read nothing aside) when that span fits the stage (huffman_dev.hip).  The
+// stage picked is the one of least modelled time, a block costing
+// (1.86 + 0.0186 * span KB) x the stage's occupancy factor (1 / 1.1 / 1.45 for
+// 16 / 12 / 8 waves per CU) x 1.9 when it does not fit and reads global
+// memory -- a fit of tools/huff_time.py's c3-shape times at 128, 192 and 320
+// kbps, the unstaged factor raised from the 1.7 of uniform batches because in
+// a mixed batch the unstaged blocks also set the launch's tail (half 128, half
+// 320 kbps: default 4.47 ms, mid 4.99, wide 4.33).
 uint32_t mp3g_huffman_stage_flags(const mp3g_hjob* jobs, uint64_t n_granules) {
   if (!jobs) return 0u;
   const uint64_t n = 2 * n_granules;
-  uint64_t fit = 0, mid = 0, wide = 0, blocks = 0;  // blocks that fit each stage
+  const uint64_t words[3] = {(uint64_t)kHuffStageWords, (uint64_t)kHuffStageWordsMid, (uint64_t)kHuffStageWordsWide};
+  const double occupancy[3] = {1.0, 1.1, 1.45}, unstaged = 1.9;
+  double cost[3] = {0.0, 0.0, 0.0};
   for (uint64_t b0 = 0; b0 < n; b0 += kHuffJobsPerBlock) {
     uint64_t lo = ~0ull, hi = 0;
     for (uint64_t j = b0; j < n && j < b0 + kHuffJobsPerBlock; j++) {
@@ -434,16 +443,14 @@ uint32_t mp3g_huffman_stage_flags(const mp3g_hjob* jobs, uint64_t n_granules) {
       lo = std::min<uint64_t>(lo, (jobs[j].part2_start - jobs[j].scf0_delta) & ~63ull);
       hi = std::max<uint64_t>(hi, jobs[j].bit_end);
     }
-    const uint64_t words = hi > lo && lo != ~0ull ? (hi - lo + 63) >> 6 : 0;
-    blocks++;
-    fit += words <= (uint64_t)kHuffStageWords;
-    mid += words <= (uint64_t)kHuffStageWordsMid;
-    wide += words <= (uint64_t)kHuffStageWordsWide;
+    const uint64_t span = hi > lo && lo != ~0ull ? (hi - lo + 63) >> 6 : 0;  // 64-bit words
+    const double work = 1.86 + 0.0186 * (double)span * 8.0 / 1024.0;
+    for (int k = 0; k < 3; k++) cost[k] += work * occupancy[k] * (span <= words[k] ? 1.0 : unstaged);
   }
-  // the smallest stage (the most waves per CU) that holds 90 % of the blocks
-  if (10 * fit >= 9 * blocks) return 0u;
-  if (10 * mid >= 9 * blocks) return MP3G_HUFF_STAGE_MID;
-  return MP3G_HUFF_STAGE_WIDE;
+  int best = 0;
+  for (int k = 1; k < 3; k++)
+    if (cost[k] < cost[best]) best = k;
+  return best == 0 ? 0u : best == 1 ? MP3G_HUFF_STAGE_MID : MP3G_HUFF_STAGE_WIDE;
 }
 
 // stamped launch of a fast plan: kFastStampSlots per chunk into h

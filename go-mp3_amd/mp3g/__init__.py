@@ -299,9 +299,9 @@ def huffman_execute(d_jobs, n_granules, d_main_data, d_granules, d_coeffs, strea
 
 
 def huffman_stage_flags(jobs, n_granules=None):
-    """mp3g_huffman_stage_flags: the smallest main-data stage (0, HUFF_STAGE_MID,
-    HUFF_STAGE_WIDE) that holds 90 % of the batch's 256-job blocks (jobs: the
-    scan's HJOB_DTYPE array, host memory)."""
+    """mp3g_huffman_stage_flags: the main-data stage (0, HUFF_STAGE_MID,
+    HUFF_STAGE_WIDE) of least modelled time for the batch's 256-job blocks
+    (jobs: the scan's HJOB_DTYPE array, host memory)."""
     jobs = np.ascontiguousarray(jobs, dtype=HJOB_DTYPE)
     n = len(jobs) // 2 if n_granules is None else int(n_granules)
     return int(lib().mp3g_huffman_stage_flags(jobs.ctypes.data, n))

@@ -304,10 +304,11 @@ int mp3g_huffman_execute(int device, const mp3g_hjob* d_jobs, uint64_t n_granule
 #define MP3G_HUFF_STAGE_MID 4u
 int mp3g_huffman_execute_ex(int device, const mp3g_hjob* d_jobs, uint64_t n_granules, const uint8_t* d_main_data,
                             mp3g_granule* d_granules, int16_t* d_coeffs, uint32_t flags, void* hip_stream);
-/* Host-side advice for mp3g_huffman_execute_ex: the smallest stage (0,
- * MP3G_HUFF_STAGE_MID or MP3G_HUFF_STAGE_WIDE) that holds 90 % of the batch's
- * 256-job blocks, else MP3G_HUFF_STAGE_WIDE.  `jobs`: the scan's jobs (host
- * memory, 2 * n_granules). */
+/* Host-side advice for mp3g_huffman_execute_ex: the stage (0,
+ * MP3G_HUFF_STAGE_MID or MP3G_HUFF_STAGE_WIDE) of least modelled time for the
+ * batch's 256-job blocks, from their main-data spans (each block staged when
+ * it fits, read from global memory otherwise; the stage's waves per CU).
+ * `jobs`: the scan's jobs (host memory, 2 * n_granules). */
 uint32_t mp3g_huffman_stage_flags(const mp3g_hjob* jobs, uint64_t n_granules);
 
 /* Bitstreams in, PCM out (the batch drop-in): scan on the host, Huffman + DSP

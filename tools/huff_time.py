@@ -54,9 +54,13 @@ def main():
     for cfg in a.configs.split(","):
         # c3hi: c3's shape at 320 kbps (bitrate index 14): main data ~2.6x c3's
         ns, nf = (1, 10000) if cfg == "c2" else (1024, 1024)
-        br = 14 if cfg == "c3hi" else 11 if cfg == "c3mid" else None  # 320 / 192 kbps
+        # c3hi / c3mid: 320 / 192 kbps; c3mix: streams alternating 128 and 320 kbps
+        # (c3most: one stream in five at 320 kbps, the rest at 128)
+        brs = {"c3hi": lambda k: 14, "c3mid": lambda k: 11, "c3mix": lambda k: 9 if k % 2 else 14,
+               "c3most": lambda k: 9 if k % 5 else 14}
+        br = brs.get(cfg, lambda k: None)
         with ThreadPoolExecutor(16) as ex:
-            datas = list(ex.map(lambda k: synth.encode_stream(1 + k, nf, bitrate_index=br), range(ns)))
+            datas = list(ex.map(lambda k: synth.encode_stream(1 + k, nf, bitrate_index=br(k)), range(ns)))
         s = mp3g.scan_streams(datas, n_threads=16)
         staged = staged_blocks(s["jobs"])
         n = len(s["granules"])
