@@ -198,3 +198,22 @@ def test_huffman_stage_advice():
     mostly = [synth.encode_stream(1 + k, 256, bitrate_index=9 if k % 5 else 14) for k in range(10)]
     s = mp3g.scan_streams(mostly, n_threads=4)
     assert mp3g.huffman_stage_flags(s["jobs"]) == 0
+
+
+@pytest.mark.parametrize("span_kb,want", [(20, 0), (38, "MID"), (60, "WIDE"), (100, 0)])
+def test_huffman_stage_advice_spans(span_kb, want):
+    """The stage advice on constructed jobs: blocks of 256 jobs spanning
+    span_kb of main data take the smallest stage that holds them, and a
+    block no stage holds keeps the default (most waves per CU)."""
+    import mp3g
+    n_blocks = 8
+    jobs = np.zeros(256 * n_blocks, mp3g.HJOB_DTYPE)
+    span_bits = span_kb * 1024 * 8
+    for b in range(n_blocks):
+        base = b * 200 * 1024 * 8
+        blk = jobs[256 * b:256 * (b + 1)]
+        blk["sf_kind"] = 1
+        blk["part2_start"] = base + np.arange(256) * (span_bits // 256)
+        blk["bit_end"] = blk["part2_start"] + span_bits // 256
+    got = mp3g.huffman_stage_flags(jobs)
+    assert got == {0: 0, "MID": mp3g.HUFF_STAGE_MID, "WIDE": mp3g.HUFF_STAGE_WIDE}[want], (span_kb, got)
