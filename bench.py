@@ -17,11 +17,14 @@ scaling: weak -- every rank decodes its own stream(s); no data-path collective
          buffer), timed and reported separately under "gather" (value stays
          the kernel-only number); --no-gather skips it.
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
-torch.distributed.run (one process per GPU; --backend nccl = RCCL, the
-default, or gloo with the collectives staged through host memory -- the
-one-GPU rehearsal of the multi-rank path, tests/test_gpu_bench_dist.py).
-Ranks map to GPUs as LOCAL_RANK modulo the visible device count.
+Launch: python bench.py [--gpus N --steps K --warmup W].  One process per
+GPU: under torch.distributed.run (WORLD_SIZE must equal N), or, with no
+launcher and N > 1, bench.py starts `torch.distributed.run --nproc-per-node N`
+itself as a child process before anything touches the GPU and passes its
+output through.  --backend nccl = RCCL (the default), or gloo with the
+collectives staged through host memory -- the one-GPU rehearsal of the
+multi-rank path, tests/test_gpu_bench_dist.py.  Ranks map to GPUs as
+LOCAL_RANK modulo the visible device count.
 """
 import argparse
 import json
@@ -84,6 +87,8 @@ def parse():
     ap.add_argument("--no-polyphase", action="store_true",
                     help="skip the standalone polyphase kernel leg (mp3g_plan_synth_execute)")
     ap.add_argument("--no-c2", action="store_true", help="c3: skip the secondary c2 object")
+    ap.add_argument("--no-hot", action="store_true",
+                    help="c3: skip the loud-input leg (fast kernel at ~1 %% and ~10 %% hot granules)")
     ap.add_argument("--parity-streams", type=int, default=128,
                     help="c3: streams whose PCM is checked against the oracle (all host threads)")
     return ap.parse_args()
@@ -300,6 +305,56 @@ def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle, pip
         want = np.frombuffer(opcm, np.int16)
         out["max_dpcm_lsb_vs_oracle"] = int(np.abs(got.astype(np.int32) - want).max()) if ost == 0 and \
             len(want) == n * 1152 else "oracle status %d" % ost
+    return out
+
+
+def hot_leg(args, rank, dev, stream, g, c, streams, local, d_c, fracs=(0.006, 0.06)):
+    """the fast mode's magnitude bound.  Granules whose
+    hybrid output exceeds it run again in the reference's operation order (the
+    hot zones).  The same c3 input with a seeded fraction of its granules made
+    loud (synth.loud_granules: global_gain + 56) so that about 1 % and 10 % of
+    the granules are hot: W untimed + K timed launches of the fast plan each,
+    HIP events on the launch stream, the fallback's own counters
+    (mp3g_plan_hot_stats) from one more launch, and rank 0 checks the first
+    16 streams of the 10 % case against the oracle (checker only)."""
+    import torch
+    import mp3g
+    from mp3g import synth
+    h = stream.cuda_stream
+    n = len(g)
+    out = []
+    d_p = torch.empty(n * 1152, dtype=torch.int16, device=dev)
+    for frac in fracs:
+        g2, mask = synth.loud_granules(g, frac, seed=7 + rank)
+        d_g2 = torch.from_numpy(g2.view(np.uint8).copy()).to(dev)
+        plan = mp3g.Plan(streams, mode=mp3g.MODE_FAST, device=local)
+        for _ in range(args.warmup):
+            plan.execute(d_g2, d_c, d_p, stream=h)
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(args.steps):
+            plan.execute(d_g2, d_c, d_p, stream=h)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        ms = e0.elapsed_time(e1) / args.steps
+        plan.hot_stats(reset=True)
+        plan.execute(d_g2, d_c, d_p, stream=h)
+        hs = plan.hot_stats()
+        plan.close()
+        r = {"loud_granules": round(float(mask.mean()), 5), "hot_fraction": round(hs["hot"] / n, 5),
+             "rerun_fraction": round(hs["run"] / n, 5), "rewritten_fraction": round(hs["rewritten"] / n, 5),
+             "kernel_ms": round(ms, 4), "frames_per_s": round(n / 2 / (ms * 1e-3), 1)}
+        if rank == 0 and not args.no_cpu_baseline and frac == fracs[-1]:
+            sys.path.insert(0, os.path.join(REPO, "oracle"))
+            import oracle  # checker of the timed output only
+            per = int(streams["n_granules"][0])
+            k = min(16, len(streams))
+            ref = oracle.dsp_streams_mt(g2[:per * k], c[:per * k], mp3g.streams_for([per] * k), CPU_THREADS)
+            r["max_dpcm_lsb"] = dpcm(d_p[:per * k * 1152].cpu().numpy().reshape(-1, 576, 2), ref)
+            r["parity_granules"] = per * k
+        out.append(r)
+        del d_g2
     return out
 
 
@@ -568,15 +623,58 @@ def dpcm(a, b):
     return int(np.abs(a.astype(np.int32) - b.astype(np.int32)).max(initial=0))
 
 
+def launch_ranks(n):
+    """`bench.py --gpus N` with no launcher around it: start N ranks with
+    torch.distributed.run as a CHILD process (never exec: this process must not
+    have touched the GPU, and it has not -- not even `import torch`), pass its
+    output through (rank 0 prints the JSON line) and return its exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"bench.py: starting {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
+
+
+def check_world(gpus, environ):
+    """The launch decision, made before anything imports torch: returns
+    'launch' (no launcher and N > 1: start N ranks), 'run' (this process is a
+    rank, or N = 1 alone), or an error message (WORLD_SIZE disagrees with
+    --gpus: a SCALE run would otherwise record the wrong N silently)."""
+    if gpus < 1:
+        return f"--gpus must be >= 1 (got {gpus})"
+    ws = environ.get("WORLD_SIZE")
+    if ws is None:
+        return "launch" if gpus > 1 else "run"
+    if int(ws) != gpus:
+        return f"--gpus {gpus} but WORLD_SIZE={ws}: the launcher and the flag disagree"
+    return "run"
+
+
 def main():
     args = parse()
+    what = check_world(args.gpus, os.environ)
+    if what == "launch":
+        sys.exit(launch_ranks(args.gpus))
+    if what != "run":
+        print("bench.py: " + what, file=sys.stderr)
+        sys.exit(2)
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     # (device_count does not initialise the GPU on this image)
-    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+    n_dev = torch.cuda.device_count()
+    if args.backend == "nccl" and world > max(1, n_dev):
+        print(f"bench.py: {world} RCCL ranks need {world} GPUs, {n_dev} visible "
+              f"(--backend gloo rehearses N ranks on fewer GPUs)", file=sys.stderr)
+        sys.exit(2)
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, n_dev)
     # a process group whenever torch.distributed.run started us, N = 1
     # included: the RCCL path (barriers, device max over ranks, the gather)
     # then runs on a one-GPU box too (tests/test_gpu_bench_dist.py)
@@ -622,6 +720,20 @@ def main():
     res = {m: measure(m) for m in modes}
     main_res = res[args.mode]
     frames_rank = n_frames
+    # the fast kernel's hot-granule fallback on the timed input itself: one
+    # more launch with the plan's counters
+    hot_timed = None
+    if "fast" in res:
+        hp_ = mp3g.Plan(streams, granules_per_chunk=args.chunk, mode=mp3g.MODE_FAST, device=local)
+        hp_.execute(d_g, d_c, d_pcm, stream=h)
+        hs = hp_.hot_stats()
+        hp_.close()
+        hot_timed = {"hot_fraction": round(hs["hot"] / n_gran, 6), "rerun_fraction": round(hs["run"] / n_gran, 6),
+                     "rewritten_fraction": round(hs["rewritten"] / n_gran, 6),
+                     "counts": hs, "source": "mp3g_plan_hot_stats after one launch of the timed input"}
+    hot_cliff = None
+    if args.config == "c3" and not args.no_hot and "fast" in res:
+        hot_cliff = hot_leg(args, rank, dev, stream, g, c, streams, local, d_c)
 
     bitstream = None
     if not args.no_bitstream and args.config in ("c2", "c3"):
@@ -710,6 +822,10 @@ def main():
         if out["roofline"]["traffic_same_build"] is False:
             print("bench.py: warning: roofline traffic is from a profile of another build (%s)" % traffic_src,
                   file=sys.stderr)
+        if hot_timed is not None:
+            out["modes"]["fast"]["hot_granules"] = hot_timed
+        if hot_cliff is not None:
+            out["modes"]["fast"]["hot_cliff"] = hot_cliff
         if gather is not None:
             out["gather_ms"] = gather["ms"]
             out["gather"] = gather

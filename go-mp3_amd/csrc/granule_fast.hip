@@ -1006,7 +1006,7 @@ __global__ void __launch_bounds__(kLanes * kWaves, MP3G_FAST_WAVES_PER_SIMD)
 granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, const mp3g_granule* __restrict__ gran,
                     const int16_t* __restrict__ coef, const mp3g_state* __restrict__ state_in,
                     mp3g_state* __restrict__ state_out, int16_t* __restrict__ pcm,
-                    unsigned long long* __restrict__ stamps) {
+                    unsigned long long* __restrict__ stamps, uint32_t* __restrict__ hot_count) {
   unsigned long long ph[kPhases] = {}, tprev = 0, rt[4] = {};
   if constexpr (kStamp) rt[0] = __builtin_amdgcn_s_memrealtime();
   auto stamp = [&](int p) {
@@ -1642,6 +1642,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     f2 zst[9];  // the zones' own overlap state (nothing flows in from the fast pass)
     uint32_t done = 0;  // the exact state in zst / the ring is valid for granules < done
     bool have = false;
+    uint32_t n_out = 0, n_run = 0, n_hot = 0;  // for hot_count (kernels.h kHotCounters)
     for (uint32_t i = 0; i < nz; i++) {
       const uint32_t zs = __builtin_amdgcn_readfirstlane(s.zone[i][0]);
       uint32_t ze = __builtin_amdgcn_readfirstlane(s.zone[i][1]);
@@ -1660,14 +1661,23 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       }
       for (; gz < ze; gz++) {
         const bool nv = replay_needs_v(gran, gz, zs);
+        n_run++;
+        n_out += gz >= zs ? 1u : 0u;
         if (exact_granule(gran, coef, pcm, s, sh, gz, gz >= zs, nv, zst)) {
           const uint32_t e = zone_end(gran, gz, end);
           ze = e > ze ? e : ze;
+          n_hot++;
         }
       }
       done = gz;
     }
     if (done >= end) export_state(zst);
+    // (rare: one vector atomic per counter from lane 0 of a chunk with zones)
+    if (hot_count && lane_fresh() == 0) {
+      atomicAdd(hot_count + 0, n_out);
+      atomicAdd(hot_count + 1, n_run);
+      atomicAdd(hot_count + 2, n_hot);
+    }
   }
   if constexpr (kStamp) {
     rt[3] = __builtin_amdgcn_s_memrealtime();

@@ -7,6 +7,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -18,6 +20,7 @@
 #include "../../include/mp3g.h"
 #include "abi_util.h"
 #include "host_parse.h"
+#include "kernels.h"
 
 using namespace mp3g;
 using host::St;
@@ -209,7 +212,41 @@ struct DevMem {
 // set in use by another thread allocates its own.
 struct PipeBufs {
   Pinned arena[2];
-  DevMem d_gran[2], d_jobs[2], d_md[2], d_coef[2], d_pcm[2];
+  DevMem d_gran[2], d_jobs[2], d_md[2], d_chunks[2], d_pcm[2], d_coef;
+  // the pipeline's streams and per-slot events (created once per device)
+  hipStream_t up = nullptr, comp = nullptr, down = nullptr;
+  hipEvent_t h2d[2] = {}, kern[2] = {}, d2h[2] = {};
+  bool ensure_sync() {
+    for (hipStream_t* q : {&up, &comp, &down})
+      if (!*q && hipStreamCreateWithFlags(q, hipStreamNonBlocking) != hipSuccess) return false;
+    for (int i = 0; i < 2; i++)
+      for (hipEvent_t* ev : {&h2d[i], &kern[i], &d2h[i]})
+        if (!*ev && hipEventCreateWithFlags(ev, hipEventDisableTiming) != hipSuccess) return false;
+    return true;
+  }
+  ~PipeBufs() {
+    for (hipStream_t q : {up, comp, down})
+      if (q) (void)hipStreamDestroy(q);
+    for (int i = 0; i < 2; i++)
+      for (hipEvent_t ev : {h2d[i], kern[i], d2h[i]})
+        if (ev) (void)hipEventDestroy(ev);
+  }
+};
+
+// MP3G_PIPE_TRACE=1: host timestamps of mp3g_decode_streams_into's stages on
+// stderr (diagnostic; tools/pipe_time.py)
+struct PipeTrace {
+  bool on;
+  std::chrono::steady_clock::time_point t0;
+  PipeTrace() : on(std::getenv("MP3G_PIPE_TRACE") != nullptr), t0(std::chrono::steady_clock::now()) {}
+  void mark(const char* what, long group = -1) const {
+    if (!on) return;
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (group >= 0)
+      std::fprintf(stderr, "mp3g pipe %9.3f ms %s %ld\n", ms, what, group);
+    else
+      std::fprintf(stderr, "mp3g pipe %9.3f ms %s\n", ms, what);
+  }
 };
 std::mutex g_pipe_mu;
 std::vector<std::unique_ptr<PipeBufs>> g_pipe;  // [device]
@@ -442,9 +479,11 @@ int mp3g_decode_streams_into(int device, uint32_t n_streams, const uint8_t* cons
     return abi_fail(MP3G_ERR_INVALID_ARGUMENT, "null argument");
   *n_granules = 0;
   const int nt = n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency();
+  const PipeTrace trace;
   // ---- the layout: a header-only pre-pass over every stream ----
   std::vector<uint64_t> pg(n_streams), pm(n_streams), g_at(n_streams + 1), m_at(n_streams + 1);
   parallel_for(0, n_streams, nt, [&](uint32_t k) { host::prescan(datas[k], lens[k], &pg[k], &pm[k]); });
+  trace.mark("prescan");
   for (uint32_t k = 0; k < n_streams; k++) {
     g_at[k + 1] = g_at[k] + pg[k];
     m_at[k + 1] = m_at[k] + ((pm[k] + 15) & ~(uint64_t)15);
@@ -480,7 +519,9 @@ int mp3g_decode_streams_into(int device, uint32_t n_streams, const uint8_t* cons
   if (!pcm) return abi_fail(MP3G_ERR_INVALID_ARGUMENT, "null pcm");
 
   // ---- groups of consecutive streams with about equal granule counts ----
-  uint32_t G = n_groups ? n_groups : (uint32_t)std::min<uint64_t>(8, std::max<uint64_t>(1, total / 65536));
+  // (~128 K granules, 300 MB of PCM each: the first group's scan and
+  // transfers are the pipeline's fill, the PCM copy-out its steady state)
+  uint32_t G = n_groups ? n_groups : (uint32_t)std::min<uint64_t>(32, std::max<uint64_t>(1, total / 131072));
   G = std::max(1u, std::min(G, n_streams));
   std::vector<uint32_t> cut{0};
   for (uint32_t k = 0; k < n_streams && cut.size() < G; k++)
@@ -492,14 +533,20 @@ int mp3g_decode_streams_into(int device, uint32_t n_streams, const uint8_t* cons
     max_ng = std::max(max_ng, g_at[cut[gi + 1]] - g_at[cut[gi]]);
     max_md = std::max(max_md, m_at[cut[gi + 1]] - m_at[cut[gi]]);
   }
-  // pinned arena per slot: [granules | jobs | main data + 16]
+  // pinned arena per slot: [granules | jobs | main data + 16 | chunk table]
+  // (a plan without state flags has at most one chunk per granule)
   const size_t b_gran = max_ng * sizeof(mp3g_granule), b_jobs = 2 * max_ng * sizeof(mp3g_hjob);
-  const size_t b_md = max_md + 16;
+  const size_t b_md = (max_md + 16 + 15) & ~(size_t)15, b_chunks = max_ng * sizeof(ChunkDesc);
+  trace.mark("layout");
 
   int prev = -1;
   (void)hipGetDevice(&prev);
   if (hipSetDevice(device) != hipSuccess) return abi_fail(MP3G_ERR_NO_DEVICE, "decode_streams_into: device");
-  int rc = MP3G_OK;
+  int rc = ensure_device_ready(device);
+  if (rc) {
+    if (prev >= 0) (void)hipSetDevice(prev);
+    return rc;
+  }
   // this device's cached buffer set, or a private one if it is in use
   std::unique_ptr<PipeBufs> own;
   PipeBufs* B = nullptr;
@@ -519,36 +566,48 @@ int mp3g_decode_streams_into(int device, uint32_t n_streams, const uint8_t* cons
     own.reset(new (std::nothrow) PipeBufs);
     B = own.get();
   }
-  if (!B) return abi_fail(MP3G_ERR_OUT_OF_MEMORY, "decode_streams_into: buffers");
+  if (!B) {
+    if (prev >= 0) (void)hipSetDevice(prev);
+    return abi_fail(MP3G_ERR_OUT_OF_MEMORY, "decode_streams_into: buffers");
+  }
   {
-    Pinned* arena = B->arena;
-    DevMem *d_gran = B->d_gran, *d_jobs = B->d_jobs, *d_md = B->d_md, *d_coef = B->d_coef, *d_pcm = B->d_pcm;
-    hipStream_t st = nullptr;
-    hipEvent_t done[2] = {nullptr, nullptr};
-    std::vector<mp3g_plan*> plans(ng_groups, nullptr);
-    hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
-    for (int i = 0; i < 2 && e == hipSuccess; i++) e = hipEventCreateWithFlags(&done[i], hipEventDisableTiming);
-    for (int i = 0; i < 2 && e == hipSuccess; i++) {
-      const bool ok = arena[i].reserve(b_gran + b_jobs + b_md) && d_gran[i].reserve(b_gran) &&
-                      d_jobs[i].reserve(b_jobs) && d_md[i].reserve(b_md) &&
-                      d_coef[i].reserve(max_ng * MP3G_COEF_PER_GRANULE * sizeof(int16_t)) &&
-                      d_pcm[i].reserve(max_ng * MP3G_PCM_BYTES_PER_GRANULE);
-      if (!ok) e = hipErrorOutOfMemory;
+    // Three streams, so that a group's PCM copy-out (the long pole: 2,304 B
+    // per granule over PCIe) runs back to back with the next group's
+    // bitstream upload (the other direction) and kernels:
+    //   up:   [wait kern(g-2)] H2D granules, jobs, main data, chunk table  -> h2d(g)
+    //   comp: [wait h2d(g), d2h(g-2)] main-data kernel, granule kernel     -> kern(g)
+    //   down: [wait kern(g)] D2H PCM into the caller's buffer              -> d2h(g)
+    // Two buffer slots (g & 1) per input / PCM buffer; the coefficients are
+    // used only on `comp`, in order, so one buffer serves every group.  The
+    // host reuses a pinned arena slot after waiting for its upload (h2d(g-2)).
+    rc = B->ensure_sync() ? MP3G_OK : abi_fail(MP3G_ERR_DEVICE, "decode_streams_into: streams / events");
+    for (int i = 0; i < 2 && rc == MP3G_OK; i++) {
+      const bool ok = B->arena[i].reserve(b_gran + b_jobs + b_md + b_chunks) && B->d_gran[i].reserve(b_gran) &&
+                      B->d_jobs[i].reserve(b_jobs) && B->d_md[i].reserve(b_md) && B->d_chunks[i].reserve(b_chunks) &&
+                      B->d_pcm[i].reserve(max_ng * MP3G_PCM_BYTES_PER_GRANULE);
+      if (!ok) rc = abi_fail(MP3G_ERR_DEVICE, "decode_streams_into: buffers");
     }
-    if (e != hipSuccess) rc = abi_fail(MP3G_ERR_DEVICE, "decode_streams_into: buffers");
+    if (rc == MP3G_OK && !B->d_coef.reserve(max_ng * MP3G_COEF_PER_GRANULE * sizeof(int16_t)))
+      rc = abi_fail(MP3G_ERR_DEVICE, "decode_streams_into: buffers");
+    trace.mark("buffers");
+    hipStream_t up = B->up, comp = B->comp, down = B->down;
+    std::vector<ChunkDesc> chunks;
     for (size_t gi = 0; gi < ng_groups && rc == MP3G_OK; gi++) {
       const int slot = (int)(gi & 1);
-      if (gi >= 2 && hipEventSynchronize(done[slot]) != hipSuccess) {  // the slot's previous group is done
+      if (gi >= 2 && hipEventSynchronize(B->h2d[slot]) != hipSuccess) {  // the arena slot's upload is done
         rc = abi_fail(MP3G_ERR_DEVICE, "decode_streams_into: device");
         break;
       }
+      trace.mark("wait arena", gi);
       const uint32_t k0 = cut[gi], k1 = cut[gi + 1];
       const uint64_t G0 = g_at[k0], M0 = m_at[k0], ng = g_at[k1] - G0, nmd = m_at[k1] - M0;
-      auto* gran = static_cast<mp3g_granule*>(arena[slot].p);
-      auto* jobs = reinterpret_cast<mp3g_hjob*>(static_cast<uint8_t*>(arena[slot].p) + b_gran);
-      uint8_t* md = static_cast<uint8_t*>(arena[slot].p) + b_gran + b_jobs;
+      uint8_t* base = static_cast<uint8_t*>(B->arena[slot].p);
+      auto* gran = reinterpret_cast<mp3g_granule*>(base);
+      auto* jobs = reinterpret_cast<mp3g_hjob*>(base + b_gran);
+      uint8_t* md = base + b_gran + b_jobs;
+      auto* h_chunks = reinterpret_cast<ChunkDesc*>(base + b_gran + b_jobs + b_md);
       // host scan of the group straight into the pinned arena (jobs address
-      // the group's main data; the previous group's transfers and kernels run
+      // the group's main data; the previous groups' transfers and kernels run
       // meanwhile)
       std::vector<mp3g_stream> local(k1 - k0);
       std::atomic<bool> holes{false}, overflow{false};
@@ -576,45 +635,64 @@ int mp3g_decode_streams_into(int device, uint32_t n_streams, const uint8_t* cons
         std::memset(md + sink.n, 0, (size_t)(m_at[k + 1] - M0 - sink.n));
       });
       std::memset(md + nmd, 0, 16);
+      trace.mark("scan", gi);
       if (overflow) {  // the pre-pass is an upper bound, so this cannot happen
         rc = abi_fail(MP3G_ERR_INVALID_ARGUMENT, "decode_streams_into: layout");
         break;
       }
-      rc = mp3g_plan_create(device, local.data(), k1 - k0, 0, mode, &plans[gi]);
+      uint64_t pn = 0, ph = 0;
+      rc = plan_chunks(device, local.data(), k1 - k0, 0, mode, &chunks, &pn, &ph);
       if (rc) break;
-      e = hipMemcpyAsync(d_gran[slot].p, gran, ng * sizeof(mp3g_granule), hipMemcpyHostToDevice, st);
+      if (chunks.size() > max_ng) {
+        rc = abi_fail(MP3G_ERR_INVALID_ARGUMENT, "decode_streams_into: chunk table");
+        break;
+      }
+      if (!chunks.empty()) std::memcpy(h_chunks, chunks.data(), chunks.size() * sizeof(ChunkDesc));
+      const uint32_t stage = mp3g_huffman_stage_flags(jobs, ng);
+      // up
+      hipError_t e = gi >= 2 ? hipStreamWaitEvent(up, B->kern[slot], 0) : hipSuccess;
+      if (e == hipSuccess) e = hipMemcpyAsync(B->d_gran[slot].p, gran, ng * sizeof(mp3g_granule), hipMemcpyHostToDevice, up);
       if (e == hipSuccess)
-        e = hipMemcpyAsync(d_jobs[slot].p, jobs, 2 * ng * sizeof(mp3g_hjob), hipMemcpyHostToDevice, st);
-      if (e == hipSuccess) e = hipMemcpyAsync(d_md[slot].p, md, nmd + 16, hipMemcpyHostToDevice, st);
+        e = hipMemcpyAsync(B->d_jobs[slot].p, jobs, 2 * ng * sizeof(mp3g_hjob), hipMemcpyHostToDevice, up);
+      if (e == hipSuccess) e = hipMemcpyAsync(B->d_md[slot].p, md, nmd + 16, hipMemcpyHostToDevice, up);
+      if (e == hipSuccess && !chunks.empty())
+        e = hipMemcpyAsync(B->d_chunks[slot].p, h_chunks, chunks.size() * sizeof(ChunkDesc), hipMemcpyHostToDevice, up);
+      if (e == hipSuccess) e = hipEventRecord(B->h2d[slot], up);
+      // comp
+      if (e == hipSuccess) e = hipStreamWaitEvent(comp, B->h2d[slot], 0);
+      if (e == hipSuccess && gi >= 2) e = hipStreamWaitEvent(comp, B->d2h[slot], 0);
       if (e == hipSuccess && holes)
-        e = hipMemsetAsync(d_pcm[slot].p, 0, ng * MP3G_PCM_BYTES_PER_GRANULE, st);
+        e = hipMemsetAsync(B->d_pcm[slot].p, 0, ng * MP3G_PCM_BYTES_PER_GRANULE, comp);
       if (e != hipSuccess) {
         rc = abi_fail(MP3G_ERR_DEVICE, "decode_streams_into: H2D");
         break;
       }
-      rc = mp3g_huffman_execute_ex(device, static_cast<const mp3g_hjob*>(d_jobs[slot].p), ng,
-                                static_cast<const uint8_t*>(d_md[slot].p), static_cast<mp3g_granule*>(d_gran[slot].p),
-                                static_cast<int16_t*>(d_coef[slot].p),
-                                (mode_reads_to_count1(mode) ? MP3G_HUFF_ROWS_COUNT1 : 0u) |
-                                    mp3g_huffman_stage_flags(jobs, ng),
-                                st);
-      if (rc == MP3G_OK)
-        rc = mp3g_plan_execute(plans[gi], static_cast<const mp3g_granule*>(d_gran[slot].p),
-                               static_cast<const int16_t*>(d_coef[slot].p), nullptr, nullptr,
-                               static_cast<int16_t*>(d_pcm[slot].p), st);
+      rc = mp3g_huffman_execute_ex(device, static_cast<const mp3g_hjob*>(B->d_jobs[slot].p), ng,
+                                   static_cast<const uint8_t*>(B->d_md[slot].p),
+                                   static_cast<mp3g_granule*>(B->d_gran[slot].p), static_cast<int16_t*>(B->d_coef.p),
+                                   (mode_reads_to_count1(mode) ? MP3G_HUFF_ROWS_COUNT1 : 0u) | stage, comp);
+      if (rc == MP3G_OK && !chunks.empty())
+        rc = plan_launch(mode, static_cast<const ChunkDesc*>(B->d_chunks[slot].p), (uint32_t)chunks.size(),
+                         static_cast<const mp3g_granule*>(B->d_gran[slot].p),
+                         static_cast<const int16_t*>(B->d_coef.p), nullptr, nullptr,
+                         static_cast<int16_t*>(B->d_pcm[slot].p), nullptr, comp);
       if (rc) break;
-      e = hipMemcpyAsync(pcm + G0 * (MP3G_PCM_BYTES_PER_GRANULE / sizeof(int16_t)), d_pcm[slot].p,
-                         ng * MP3G_PCM_BYTES_PER_GRANULE, hipMemcpyDeviceToHost, st);
-      if (e == hipSuccess) e = hipEventRecord(done[slot], st);
+      e = hipEventRecord(B->kern[slot], comp);
+      // down
+      if (e == hipSuccess) e = hipStreamWaitEvent(down, B->kern[slot], 0);
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(pcm + G0 * (MP3G_PCM_BYTES_PER_GRANULE / sizeof(int16_t)), B->d_pcm[slot].p,
+                           ng * MP3G_PCM_BYTES_PER_GRANULE, hipMemcpyDeviceToHost, down);
+      if (e == hipSuccess) e = hipEventRecord(B->d2h[slot], down);
       if (e != hipSuccess) rc = abi_fail(MP3G_ERR_DEVICE, "decode_streams_into: D2H");
+      trace.mark("enqueue", gi);
     }
-    if (st && hipStreamSynchronize(st) != hipSuccess && rc == MP3G_OK)
-      rc = abi_fail(MP3G_ERR_DEVICE, "decode_streams_into: device");
-    for (mp3g_plan* p : plans)
-      if (p) mp3g_plan_destroy(p);
-    for (hipEvent_t ev : done)
-      if (ev) (void)hipEventDestroy(ev);
-    if (st) (void)hipStreamDestroy(st);
+    // (on an error too: nothing may still write into the caller's buffer or
+    // read the arena after return)
+    for (hipStream_t q : {up, comp, down})
+      if (q && hipStreamSynchronize(q) != hipSuccess && rc == MP3G_OK)
+        rc = abi_fail(MP3G_ERR_DEVICE, "decode_streams_into: device");
+    trace.mark("drain");
   }
   if (!own) {
     std::lock_guard<std::mutex> lk(g_pipe_mu);

@@ -35,10 +35,16 @@ constexpr int kVariantV2 = 2;
 constexpr int kVariantFast = 3;
 // exact mode v4 (default): one wave per chunk, the reference's operation order
 constexpr int kVariantExact4 = 4;
+// d_hot: kHotCounters counters the fast kernel adds its hot-granule work to
+// (or null; the other kernels ignore it)
 hipError_t launch_granule(int variant, const ChunkDesc* d_chunks, uint32_t n_chunks,
                           const mp3g_granule* d_gran, const int16_t* d_coef,
                           const mp3g_state* d_state_in, mp3g_state* d_state_out, int16_t* d_pcm,
-                          hipStream_t stream);
+                          uint32_t* d_hot, hipStream_t stream);
+// The fast kernel's hot-granule counters (granule_fast.hip): [0] granules
+// whose PCM the reference-order pass rewrote, [1] granules it ran (with the
+// replays of their entry state), [2] hot granules it met.
+constexpr int kHotCounters = 4;
 
 // Chunks of `variant` resident per CU (one per wave for the fast kernel, one
 // per workgroup for the exact kernels), from the kernel's VGPR / LDS usage.
@@ -74,7 +80,7 @@ hipError_t upload_fast_tables(const FastTables& fast, const float* req);
 hipError_t fast_kernel_attributes(hipFuncAttributes* a, int* waves_per_block);
 hipError_t launch_fast(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_granule* d_gran,
                        const int16_t* d_coef, const mp3g_state* d_state_in, mp3g_state* d_state_out,
-                       int16_t* d_pcm, unsigned long long* d_stamps, hipStream_t stream);
+                       int16_t* d_pcm, unsigned long long* d_stamps, uint32_t* d_hot, hipStream_t stream);
 
 // Exact mode v4 (granule_wexact.hip, same TU as the fast kernel).
 hipError_t wexact_kernel_attributes(hipFuncAttributes* a, int* waves_per_block);

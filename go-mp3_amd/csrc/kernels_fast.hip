@@ -47,15 +47,15 @@ hipError_t fast_kernel_attributes(hipFuncAttributes* a, int* waves_per_block) {
 
 hipError_t launch_fast(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_granule* d_gran,
                        const int16_t* d_coef, const mp3g_state* d_state_in, mp3g_state* d_state_out,
-                       int16_t* d_pcm, unsigned long long* d_stamps, hipStream_t stream) {
+                       int16_t* d_pcm, unsigned long long* d_stamps, uint32_t* d_hot, hipStream_t stream) {
   if (n_chunks == 0) return hipSuccess;
   const dim3 grid((n_chunks + v3::kWaves - 1) / v3::kWaves), block(64 * v3::kWaves);
   if (d_stamps)
     hipLaunchKernelGGL(v3::granule_fast_kernel<true>, grid, block, 0, stream, d_chunks, n_chunks, d_gran, d_coef,
-                       d_state_in, d_state_out, d_pcm, d_stamps);
+                       d_state_in, d_state_out, d_pcm, d_stamps, d_hot);
   else
     hipLaunchKernelGGL(v3::granule_fast_kernel<false>, grid, block, 0, stream, d_chunks, n_chunks, d_gran, d_coef,
-                       d_state_in, d_state_out, d_pcm, nullptr);
+                       d_state_in, d_state_out, d_pcm, nullptr, d_hot);
   return hipGetLastError();
 }
 
@@ -86,7 +86,7 @@ hipError_t launch_synth(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g
 hipError_t launch_fast_stamped(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_granule* d_gran,
                                const int16_t* d_coef, const mp3g_state* d_state_in, mp3g_state* d_state_out,
                                int16_t* d_pcm, unsigned long long* d_stamps, hipStream_t stream) {
-  return launch_fast(d_chunks, n_chunks, d_gran, d_coef, d_state_in, d_state_out, d_pcm, d_stamps, stream);
+  return launch_fast(d_chunks, n_chunks, d_gran, d_coef, d_state_in, d_state_out, d_pcm, d_stamps, nullptr, stream);
 }
 
 }  // namespace mp3g

@@ -174,12 +174,100 @@ std::vector<uint64_t> auto_chunks(const mp3g_stream* streams, uint32_t n_streams
 
 int mp3g::abi_fail(int status, const char* what) { return fail(status, what); }
 
+int mp3g::ensure_device_ready(int device) {
+  DeviceGuard guard(device);
+  if (guard.err != hipSuccess) return fail(MP3G_ERR_NO_DEVICE, "hipSetDevice", guard.err);
+  return ensure_device(device);
+}
+
+// The chunk table of a plan (chunks per stream from granules_per_chunk: 0 =
+// the cost model, bit 31 = a total chunk count spread over the streams, else
+// the length), after the checks of mp3g_plan_create; the device's tables are
+// uploaded on first use.
+int mp3g::plan_chunks(int device, const mp3g_stream* streams, uint32_t n_streams, uint32_t granules_per_chunk,
+                      uint32_t mode, std::vector<ChunkDesc>* chunks, uint64_t* n_granules, uint64_t* n_halo) {
+  if (n_streams && !streams) return fail(MP3G_ERR_INVALID_ARGUMENT, "null argument");
+  const uint32_t base_mode = mode & 0xffu;
+  if (base_mode != MP3G_MODE_EXACT && base_mode != MP3G_MODE_FAST)
+    return fail(MP3G_ERR_UNSUPPORTED, "mode not available");
+  if (mode & MP3G_FLAG_KERNEL_V1) return fail(MP3G_ERR_UNSUPPORTED, "the v1 exact kernel was retired (ABI 3)");
+  for (uint32_t s = 0; s < n_streams; s++) {
+    // the one-wave kernels (fast v3, exact v4) index granules with 32-bit
+    // wave-uniform scalars
+    const int v = plan_variant(mode);
+    if ((v == kVariantFast || v == kVariantExact4) && streams[s].first_granule + streams[s].n_granules >= (1ull << 32))
+      return fail(MP3G_ERR_UNSUPPORTED, "granule index >= 2^32 (use MP3G_FLAG_KERNEL_V2 in exact mode)");
+  }
+  DeviceGuard guard(device);
+  if (guard.err != hipSuccess) return fail(MP3G_ERR_NO_DEVICE, "hipSetDevice", guard.err);
+  int st = ensure_device(device);
+  if (st) return st;
+  // chunks per stream (lengths within a stream differ by at most one)
+  std::vector<uint64_t> nc;
+  if (granules_per_chunk == 0) {
+    nc = auto_chunks(streams, n_streams, device, mode);
+  } else if (granules_per_chunk & 0x80000000u) {
+    nc = spread_chunks(streams, n_streams, std::max<uint32_t>(1, granules_per_chunk & 0x7fffffffu));
+  } else {
+    nc.resize(n_streams);
+    for (uint32_t s = 0; s < n_streams; s++)
+      nc[s] = (streams[s].n_granules + granules_per_chunk - 1) / granules_per_chunk;
+  }
+  // ChunkDesc::n_out is 32-bit: a stream cut into too few chunks is refused
+  for (uint32_t s = 0; s < n_streams; s++)
+    if (streams[s].n_granules && (nc[s] == 0 || (streams[s].n_granules + nc[s] - 1) / nc[s] >= (1ull << 32)))
+      return fail(MP3G_ERR_UNSUPPORTED, "chunk of >= 2^32 granules");
+  chunks->clear();
+  *n_granules = *n_halo = 0;
+  for (uint32_t s = 0; s < n_streams; s++) {
+    const mp3g_stream& S = streams[s];
+    const uint64_t cs = nc[s];
+    for (uint64_t i = 0, off = 0; i < cs && off < S.n_granules; i++) {
+      // chunk i of cs: granules [i n / cs, (i + 1) n / cs)
+      const uint64_t next = (i + 1) * S.n_granules / cs;
+      ChunkDesc c{};
+      c.out_first = S.first_granule + off;
+      c.stream_first = S.first_granule;
+      c.n_out = (uint32_t)(next - off);
+      c.stream = s;
+      c.flags = (S.flags & MP3G_STREAM_STATE_IN) ? kChunkStateIn : 0u;
+      if ((S.flags & MP3G_STREAM_STATE_OUT) && off + c.n_out == S.n_granules) c.flags |= kChunkStateOut;
+      chunks->push_back(c);
+      *n_granules += c.n_out;
+      *n_halo += std::min<uint64_t>(off, 2);
+      off = next;
+    }
+    if (S.n_granules == 0 && (S.flags & MP3G_STREAM_STATE_OUT)) {
+      // empty stream exporting state: state_out = state_in (or zero)
+      ChunkDesc c{};
+      c.out_first = S.first_granule;
+      c.stream_first = S.first_granule;
+      c.n_out = 0;
+      c.stream = s;
+      c.flags = kChunkStateOut | ((S.flags & MP3G_STREAM_STATE_IN) ? kChunkStateIn : 0u);
+      chunks->push_back(c);
+    }
+  }
+  return MP3G_OK;
+}
+
+// Launch of a chunk table already on the device (d_hot: the fast kernel's
+// hot-granule counters, or null).
+int mp3g::plan_launch(uint32_t mode, const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_granule* d_gran,
+                      const int16_t* d_coef, const mp3g_state* d_state_in, mp3g_state* d_state_out, int16_t* d_pcm,
+                      uint32_t* d_hot, hipStream_t stream) {
+  HIP_TRY(launch_granule(plan_variant(mode), d_chunks, n_chunks, d_gran, d_coef, d_state_in, d_state_out, d_pcm,
+                         d_hot, stream));
+  return MP3G_OK;
+}
+
 struct mp3g_plan {
   int device = 0;
   uint32_t mode = 0;
   uint32_t n_streams = 0;
   std::vector<ChunkDesc> chunks;
-  ChunkDesc* d_chunks = nullptr;
+  ChunkDesc* d_chunks = nullptr;  // the chunk table, then kHotCounters counters (d_hot)
+  uint32_t* d_hot = nullptr;
   uint64_t n_granules = 0;
   uint64_t n_halo = 0;
 };
@@ -264,85 +352,34 @@ int mp3g_validate(const mp3g_granule* g, const int16_t* coef, uint64_t n, uint64
 
 int mp3g_plan_create(int device, const mp3g_stream* streams, uint32_t n_streams,
                      uint32_t granules_per_chunk, uint32_t mode, mp3g_plan** out_plan) {
-  if (!out_plan || (n_streams && !streams)) return fail(MP3G_ERR_INVALID_ARGUMENT, "null argument");
+  if (!out_plan) return fail(MP3G_ERR_INVALID_ARGUMENT, "null argument");
   *out_plan = nullptr;
-  const uint32_t base_mode = mode & 0xffu;
-  if (base_mode != MP3G_MODE_EXACT && base_mode != MP3G_MODE_FAST)
-    return fail(MP3G_ERR_UNSUPPORTED, "mode not available");
-  if (mode & MP3G_FLAG_KERNEL_V1) return fail(MP3G_ERR_UNSUPPORTED, "the v1 exact kernel was retired (ABI 3)");
-  for (uint32_t s = 0; s < n_streams; s++) {
-    // the one-wave kernels (fast v3, exact v4) index granules with 32-bit
-    // wave-uniform scalars
-    const int v = plan_variant(mode);
-    if ((v == kVariantFast || v == kVariantExact4) && streams[s].first_granule + streams[s].n_granules >= (1ull << 32))
-      return fail(MP3G_ERR_UNSUPPORTED, "granule index >= 2^32 (use MP3G_FLAG_KERNEL_V2 in exact mode)");
-  }
-  DeviceGuard guard(device);
-  if (guard.err != hipSuccess) return fail(MP3G_ERR_NO_DEVICE, "hipSetDevice", guard.err);
-  int st = ensure_device(device);
-  if (st) return st;
-  // chunks per stream (lengths within a stream differ by at most one)
-  std::vector<uint64_t> nc;
-  if (granules_per_chunk == 0) {
-    nc = auto_chunks(streams, n_streams, device, mode);
-  } else if (granules_per_chunk & 0x80000000u) {
-    nc = spread_chunks(streams, n_streams, std::max<uint32_t>(1, granules_per_chunk & 0x7fffffffu));
-  } else {
-    nc.resize(n_streams);
-    for (uint32_t s = 0; s < n_streams; s++)
-      nc[s] = (streams[s].n_granules + granules_per_chunk - 1) / granules_per_chunk;
-  }
-  // ChunkDesc::n_out is 32-bit: a stream cut into too few chunks is refused
-  for (uint32_t s = 0; s < n_streams; s++)
-    if (streams[s].n_granules && (nc[s] == 0 || (streams[s].n_granules + nc[s] - 1) / nc[s] >= (1ull << 32)))
-      return fail(MP3G_ERR_UNSUPPORTED, "chunk of >= 2^32 granules");
   mp3g_plan* p = new (std::nothrow) mp3g_plan;
   if (!p) return fail(MP3G_ERR_OUT_OF_MEMORY, "plan");
+  int st = mp3g::plan_chunks(device, streams, n_streams, granules_per_chunk, mode, &p->chunks, &p->n_granules,
+                             &p->n_halo);
+  if (st) {
+    delete p;
+    return st;
+  }
   p->device = device;
   p->mode = mode;
   p->n_streams = n_streams;
-  for (uint32_t s = 0; s < n_streams; s++) {
-    const mp3g_stream& S = streams[s];
-    const uint64_t cs = nc[s];
-    for (uint64_t i = 0, off = 0; i < cs && off < S.n_granules; i++) {
-      // chunk i of cs: granules [i n / cs, (i + 1) n / cs)
-      const uint64_t next = (i + 1) * S.n_granules / cs;
-      ChunkDesc c{};
-      c.out_first = S.first_granule + off;
-      c.stream_first = S.first_granule;
-      c.n_out = (uint32_t)(next - off);
-      c.stream = s;
-      c.flags = (S.flags & MP3G_STREAM_STATE_IN) ? kChunkStateIn : 0u;
-      if ((S.flags & MP3G_STREAM_STATE_OUT) && off + c.n_out == S.n_granules) c.flags |= kChunkStateOut;
-      p->chunks.push_back(c);
-      p->n_granules += c.n_out;
-      p->n_halo += std::min<uint64_t>(off, 2);
-      off = next;
-    }
-    if (S.n_granules == 0 && (S.flags & MP3G_STREAM_STATE_OUT)) {
-      // empty stream exporting state: state_out = state_in (or zero)
-      ChunkDesc c{};
-      c.out_first = S.first_granule;
-      c.stream_first = S.first_granule;
-      c.n_out = 0;
-      c.stream = s;
-      c.flags = kChunkStateOut | ((S.flags & MP3G_STREAM_STATE_IN) ? kChunkStateIn : 0u);
-      p->chunks.push_back(c);
-    }
+  DeviceGuard guard(device);
+  // the chunk table, and the fast kernel's hot-granule counters after it
+  const size_t tb = p->chunks.size() * sizeof(ChunkDesc);
+  hipError_t e = hipMalloc(&p->d_chunks, tb + kHotCounters * sizeof(uint32_t));
+  if (e != hipSuccess) {
+    delete p;
+    return fail(MP3G_ERR_OUT_OF_MEMORY, "hipMalloc(chunks)", e);
   }
-  if (!p->chunks.empty()) {
-    hipError_t e = hipMalloc(&p->d_chunks, p->chunks.size() * sizeof(ChunkDesc));
-    if (e != hipSuccess) {
-      delete p;
-      return fail(MP3G_ERR_OUT_OF_MEMORY, "hipMalloc(chunks)", e);
-    }
-    e = hipMemcpy(p->d_chunks, p->chunks.data(), p->chunks.size() * sizeof(ChunkDesc),
-                  hipMemcpyHostToDevice);
-    if (e != hipSuccess) {
-      (void)hipFree(p->d_chunks);
-      delete p;
-      return fail(MP3G_ERR_DEVICE, "hipMemcpy(chunks)", e);
-    }
+  p->d_hot = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(p->d_chunks) + tb);
+  if (tb) e = hipMemcpy(p->d_chunks, p->chunks.data(), tb, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemset(p->d_hot, 0, kHotCounters * sizeof(uint32_t));
+  if (e != hipSuccess) {
+    (void)hipFree(p->d_chunks);
+    delete p;
+    return fail(MP3G_ERR_DEVICE, "hipMemcpy(chunks)", e);
   }
   *out_plan = p;
   return MP3G_OK;
@@ -377,8 +414,23 @@ int mp3g_plan_execute(mp3g_plan* p, const mp3g_granule* d_gran, const int16_t* d
   for (const ChunkDesc& c : p->chunks) {
     if ((c.flags & kChunkStateOut) && !d_state_out) return fail(MP3G_ERR_INVALID_ARGUMENT, "state_out needed");
   }
-  HIP_TRY(launch_granule(plan_variant(p->mode), p->d_chunks, (uint32_t)p->chunks.size(), d_gran, d_coef, d_state_in,
-                         d_state_out, d_pcm, static_cast<hipStream_t>(hip_stream)));
+  return plan_launch(p->mode, p->d_chunks, (uint32_t)p->chunks.size(), d_gran, d_coef, d_state_in, d_state_out, d_pcm,
+                     p->d_hot, static_cast<hipStream_t>(hip_stream));
+}
+
+// The fast kernel's hot-granule counters of this plan, summed over its
+// launches since creation or the last reset (granule_fast.hip: granules whose
+// PCM the reference-order pass rewrote, granules it ran including the replay
+// of their entry state, and hot granules it met).  Synchronous.
+int mp3g_plan_hot_stats(mp3g_plan* p, uint64_t* out3, int reset) {
+  if (!p || !out3) return fail(MP3G_ERR_INVALID_ARGUMENT, "null argument");
+  DeviceGuard guard(p->device);
+  if (guard.err != hipSuccess) return fail(MP3G_ERR_NO_DEVICE, "hipSetDevice", guard.err);
+  uint32_t h[kHotCounters] = {};
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(h, p->d_hot, sizeof(h), hipMemcpyDeviceToHost));
+  for (int i = 0; i < 3; i++) out3[i] = h[i];
+  if (reset) HIP_TRY(hipMemset(p->d_hot, 0, sizeof(h)));
   return MP3G_OK;
 }
 

@@ -92,6 +92,7 @@ def lib():
         L.mp3g_plan_info.argtypes = [vp, C.POINTER(u64), C.POINTER(u64), C.POINTER(u64)]
         L.mp3g_plan_execute.argtypes = [vp, vp, vp, vp, vp, vp, vp]
         L.mp3g_plan_synth_execute.argtypes = [vp, vp, vp, vp, vp, vp, vp]
+        L.mp3g_plan_hot_stats.argtypes = [vp, C.POINTER(u64), C.c_int]
         L.mp3g_decode_host.argtypes = [C.c_int, vp, vp, u64, vp, u32, vp, vp, vp, u32]
         L.mp3g_plan_debug_phases.argtypes = [vp, vp, vp, vp, C.POINTER(u64), vp]
         L.mp3g_plan_debug_timeline.argtypes = [vp, vp, vp, vp, C.POINTER(u64), vp]
@@ -599,6 +600,15 @@ class Plan:
         _check(lib().mp3g_plan_synth_execute(self._h, p(d_gran), p(d_lines), p(d_state_in),
                                              p(d_state_out), p(d_pcm),
                                              C.c_void_p(stream) if stream else None))
+
+    def hot_stats(self, reset=False):
+        """Fast plans: the hot-granule fallback's work summed over this plan's
+        launches (mp3g_plan_hot_stats, synchronous): granules whose PCM the
+        reference-order pass rewrote, granules it ran (with the replays of
+        their entry state), hot granules it met."""
+        out = (C.c_uint64 * 3)()
+        _check(lib().mp3g_plan_hot_stats(self._h, out, 1 if reset else 0))
+        return {"rewritten": out[0], "run": out[1], "hot": out[2]}
 
     PHASES = ("params", "requantize", "stereo+antialias", "imdct", "S rows (transpose)",
               "dct32 (matrixing)", "window+store", "history")

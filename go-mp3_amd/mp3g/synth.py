@@ -267,3 +267,18 @@ def encode_batch(seeds, n_frames, n_threads=16, **kw):
     with ThreadPoolExecutor(n_threads) as ex:  # ctypes releases the GIL
         datas = list(ex.map(one, range(len(seeds))))
     return datas, g, c, streams_for([per] * len(seeds))
+
+
+def loud_granules(g, frac, seed=1, boost=56):
+    """Loud content for the fast mode's magnitude bound:
+    a seeded fraction `frac` of the granules gets its global_gain raised by
+    `boost` (capped at 255; +56 = 2^14 in amplitude), which drives their
+    hybrid output far above kHotS -- those granules run in the reference's
+    operation order.  Returns (granules copy, boosted mask)."""
+    rng = np.random.default_rng(seed)
+    mask = rng.random(len(g)) < frac
+    g = g.copy()
+    gg = g["ch"]["global_gain"].astype(np.int32)
+    gg[mask] = np.minimum(gg[mask] + boost, 255)
+    g["ch"]["global_gain"] = gg.astype(np.uint8)
+    return g, mask

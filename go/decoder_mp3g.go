@@ -14,8 +14,9 @@
 // (source.go:99-122) -- a live stream that has not ended gets a decoder and
 // every frame that has arrived.
 //
-// Written from include/mp3g.h (ABI version 3); tests/test_cgo_shim_cpu.py
-// checks every C identifier used here against the header.
+// Written from include/mp3g.h (ABI version 5, checked against the loaded
+// library by checkABI); tests/test_cgo_shim_cpu.py checks every C identifier
+// used here against the header.
 package mp3
 
 /*
@@ -34,10 +35,28 @@ import (
 	"errors"
 	"fmt"
 	"io"
+	"runtime"
 	"runtime/cgo"
+	"sync"
 	"time"
 	"unsafe"
 )
+
+// ABIVersion is the C-ABI version this shim was written against.
+const ABIVersion = 5
+
+var abiOnce sync.Once
+var abiErr error
+
+// checkABI: the loaded libmp3g must speak the ABI this file was written for.
+func checkABI() error {
+	abiOnce.Do(func() {
+		if v := int(C.mp3g_abi_version()); v != ABIVersion {
+			abiErr = fmt.Errorf("mp3: shim written for libmp3g ABI %d, library has %d", ABIVersion, v)
+		}
+	})
+	return abiErr
+}
 
 // Mode: bit-exact PCM or within +-1 LSB of the reference (faster).
 var Mode C.uint32_t = C.MP3G_MODE_EXACT
@@ -113,6 +132,9 @@ func mp3gGoSeek(h C.uintptr_t, off C.int64_t, whence C.int) C.int64_t {
 // the library calls back into r as it needs bytes and never retains a Go
 // pointer (the callbacks get a cgo.Handle).
 func NewDecoder(r io.Reader) (*Decoder, error) {
+	if err := checkABI(); err != nil {
+		return nil, err
+	}
 	rs := &readerState{r: r}
 	seekable := C.int(0)
 	if s, ok := r.(io.Seeker); ok {
@@ -126,12 +148,24 @@ func NewDecoder(r io.Reader) (*Decoder, error) {
 		h.Delete()
 		return nil, err
 	}
-	return &Decoder{d: d, h: h, rs: rs}, nil
+	return track(&Decoder{d: d, h: h, rs: rs}), nil
+}
+
+// track: the reference's Decoder has no Close (decode.go:34-43), so a drop-in
+// caller never calls it -- a finalizer releases the library decoder (its
+// pinned host and device buffers) and the handle that pins the caller's
+// reader once the Decoder is unreachable.  Close stays idempotent.
+func track(d *Decoder) *Decoder {
+	runtime.SetFinalizer(d, func(d *Decoder) { d.Close() })
+	return d
 }
 
 // NewDecoderBytes decodes a complete stream already in memory (the library
 // copies it; no callbacks): seekable as for a bytes.Reader.
 func NewDecoderBytes(data []byte, seekable bool) (*Decoder, error) {
+	if err := checkABI(); err != nil {
+		return nil, err
+	}
 	var p *C.uint8_t
 	if len(data) > 0 {
 		p = (*C.uint8_t)(unsafe.Pointer(&data[0]))
@@ -144,7 +178,7 @@ func NewDecoderBytes(data []byte, seekable bool) (*Decoder, error) {
 	if st := C.mp3g_decoder_new(p, C.size_t(len(data)), s, 0, Mode, &d); st != C.MP3G_OK {
 		return nil, statusError(st)
 	}
-	return &Decoder{d: d}, nil
+	return track(&Decoder{d: d}), nil
 }
 
 // statusError with the reader's own error for MP3G_ERR_READ.
@@ -157,8 +191,10 @@ func (rs *readerState) statusError(st C.int) error {
 
 func (d *Decoder) statusError(st C.int) error { return d.rs.statusError(st) }
 
-// Close releases the decoder's host and device memory.
+// Close releases the decoder's host and device memory (idempotent; the
+// finalizer calls it too).
 func (d *Decoder) Close() error {
+	runtime.SetFinalizer(d, nil)
 	if d.d != nil {
 		C.mp3g_decoder_free(d.d)
 		d.d = nil
@@ -253,6 +289,12 @@ func DecodeMany(files [][]byte) ([][]byte, []error) {
 	n := len(files)
 	out, errs := make([][]byte, n), make([]error, n)
 	if n == 0 {
+		return out, errs
+	}
+	if err := checkABI(); err != nil {
+		for i := range errs {
+			errs[i] = err
+		}
 		return out, errs
 	}
 	datas := (*[1 << 30]*C.uint8_t)(C.malloc(C.size_t(n) * C.size_t(unsafe.Sizeof(uintptr(0)))))[:n:n]

@@ -12,7 +12,7 @@
 // row a10) into the C-ABI's granule descriptors (include/mp3g.h
 // mp3g_granule) and the integer MainData.Is values into int16 coefficients.
 //
-// Written from include/mp3g.h (ABI version 3) field by field;
+// Written from include/mp3g.h (ABI version 5) field by field;
 // tests/test_cgo_shim_cpu.py checks every C identifier used here against the
 // header (no Go toolchain in the build image).  INTEGRATION.md explains the
 // read-ahead in decode.go that drives it.
@@ -32,7 +32,7 @@ import (
 )
 
 // ABIVersion is the C-ABI version this shim was written against.
-const ABIVersion = 4
+const ABIVersion = 5
 
 // Batch collects parsed frames; DecodeBatch replaces calling Decode() on each.
 // Not safe for concurrent use (like Decoder, decode.go:31-33).

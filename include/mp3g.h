@@ -34,8 +34,12 @@ extern "C" {
  *    out-parameter (version 1 returned the offset); the fast-mode hot-granule
  *    fallback (no signature change).
  * 3: streaming input -- mp3g_reader + mp3g_decoder_new_reader, MP3G_ERR_READ;
- *    MP3G_FLAG_KERNEL_V1 retired. */
-#define MP3G_ABI_VERSION 4
+ *    MP3G_FLAG_KERNEL_V1 retired.
+ * 4: main-data kernel stages for high bitrates -- MP3G_HUFF_STAGE_MID /
+ *    MP3G_HUFF_STAGE_WIDE flags of mp3g_huffman_execute_ex and the advice
+ *    mp3g_huffman_stage_flags.
+ * 5: mp3g_plan_hot_stats (the fast kernel's hot-granule fallback counters). */
+#define MP3G_ABI_VERSION 5
 
 /* ---- status codes ------------------------------------------------------ */
 typedef enum mp3g_status {
@@ -192,6 +196,16 @@ int mp3g_plan_execute(mp3g_plan* plan, const mp3g_granule* d_granules,
 int mp3g_plan_synth_execute(mp3g_plan* plan, const mp3g_granule* d_granules,
                             const float* d_lines, const mp3g_state* d_state_in,
                             mp3g_state* d_state_out, int16_t* d_pcm, void* hip_stream);
+
+/* Fast-mode plans: the work of the hot-granule fallback (granules whose
+ * hybrid output exceeds the fast transforms' magnitude bound run again in the
+ * reference's operation order), summed over the plan's
+ * launches since creation or the last reset.  out3[0]: granules whose PCM that
+ * pass rewrote; out3[1]: granules it ran, the replays of their entry state
+ * included; out3[2]: hot granules it met.  Synchronises the device; reset != 0
+ * zeroes the counters after reading.  (Exact-mode plans: always 0.)  No
+ * reference counterpart: go-mp3 has one arithmetic (frame.go:140-688). */
+int mp3g_plan_hot_stats(mp3g_plan* plan, uint64_t* out3, int reset);
 
 /* ---- synchronous host-buffer decode (the cgo drop-in entry) --------------
  * Copies the batch to `device`, decodes it and copies PCM (and state_out)

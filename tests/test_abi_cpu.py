@@ -75,7 +75,7 @@ def test_struct_layouts_match_c(tmp_path):
 
 def test_status_strings_and_version():
     L = mp3g.lib()
-    assert L.mp3g_abi_version() == 4
+    assert L.mp3g_abi_version() == 5
     for s in range(12):
         assert L.mp3g_status_string(s) and L.mp3g_status_string(s) != b"unknown status"
 

@@ -131,7 +131,27 @@ def test_struct_fields_written_by_the_shim_exist():
 
 def test_abi_version_matches():
     v = int(re.search(r"#define MP3G_ABI_VERSION (\d+)", HEADER).group(1))
-    assert f"const ABIVersion = {v}" in GO["frame_mp3g.go"]
+    for f in ("frame_mp3g.go", "decoder_mp3g.go"):
+        assert f"const ABIVersion = {v}" in GO[f], f
+        assert f"ABI version {v}" in GO[f], f  # the header comment
+    # both shims check the loaded library's version before using it
+    assert "C.mp3g_abi_version()" in GO["frame_mp3g.go"]
+    go = GO["decoder_mp3g.go"]
+    assert re.search(r"C\.mp3g_abi_version\(\)\); v != ABIVersion", go)
+    for fn in ("func NewDecoder(", "func NewDecoderBytes(", "func DecodeMany("):
+        body = go[go.index(fn):]
+        body = body[:body.index("\n}\n")]
+        assert "checkABI()" in body, fn
+
+
+def test_decoder_finalizer():
+    """The reference Decoder has no Close (decode.go:34-43): the shim's
+    decoders are released by a finalizer; Close clears it (idempotent)."""
+    go = GO["decoder_mp3g.go"]
+    assert "runtime.SetFinalizer(d, func(d *Decoder) { d.Close() })" in go
+    assert go.count("return track(&Decoder{") == 2
+    close_body = go[go.index("func (d *Decoder) Close() error {"):]
+    assert "runtime.SetFinalizer(d, nil)" in close_body[:close_body.index("\n}\n")]
 
 
 def test_streaming_reader_trampolines():

@@ -51,6 +51,24 @@ def test_bench_two_ranks_gloo(config):
     assert "cpu_baseline" not in d  # an N = 1 figure
 
 
+def test_bench_gpus_flag_launches_ranks():
+    """Plain `bench.py --gpus 2` (no launcher): bench.py starts the two ranks
+    itself; gloo, so both share cuda:0."""
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--config", "c2", "--backend", "gloo", "--single-mode", "--no-bitstream", "--no-polyphase"]
+    env = dict(os.environ, OMP_NUM_THREADS="4")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=REPO, env=env)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert r.returncode == 0 and len(lines) == 1, r.stdout[-3000:] + r.stderr[-5000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2
+    assert d["gather"]["bytes"] == 2 * 20000 * 2304 and d["gather_ms"] > 0
+    assert d["gather"]["parity"]["max_dpcm_lsb"] <= 1
+    assert d["max_dpcm_lsb"] <= 1
+
+
 def test_bench_one_rank_rccl():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),

@@ -293,3 +293,43 @@ def test_fast_hot_zones_across_channel_switches(gpu, pattern):
         assert_close(pcm, want, f"{pattern} chunk={chunk}")
         assert np.array_equal(pcm, serial), f"{pattern} chunk={chunk} differs from the serial run"
         assert so.tobytes() == so_serial.tobytes(), f"{pattern} chunk={chunk}: exported state differs"
+
+
+@pytest.mark.parametrize("frac", [0.006, 0.06])
+def test_fast_loud_batch_and_hot_counters(gpu, frac):
+    """Loud content: a seeded share of a c3-like batch's
+    granules made loud (synth.loud_granules: ~1 % and ~10 % hot granules)
+    stays within 1 LSB of the oracle, and the plan's hot-granule counters
+    (mp3g_plan_hot_stats) count what the kernel redid: at least every
+    boosted granule that is hot by the reference's own hybrid output, the
+    re-run covering the rewritten granules plus their replays."""
+    import torch
+    _, g, c, s = synth.encode_batch(range(40, 56), 128, n_threads=4)
+    g, mask = synth.loud_granules(g, frac, seed=11)
+    want, _ = oracle.dsp_streams(g, c, s)
+    lines = oracle.hybrid_streams(g, c, s)
+    L = np.abs(lines.reshape(len(g), 2, 32, 18))
+    L[((g["header"] >> 6) & 3) == 3, 1] = 0
+    hot_ref = (L.max(axis=(1, 2, 3)) > 4) & (L.sum(axis=2).max(axis=(1, 2)) > 64)
+    n = len(g)
+    d_g = torch.from_numpy(g.view(np.uint8).copy()).cuda()
+    d_c = torch.from_numpy(c.view(np.uint8).reshape(-1).copy()).cuda()
+    d_p = torch.zeros(n * 2304, dtype=torch.uint8, device="cuda")
+    plan = gpu.Plan(s, mode=gpu.MODE_FAST)
+    assert plan.hot_stats() == {"rewritten": 0, "run": 0, "hot": 0}
+    plan.execute(d_g, d_c, d_p, stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    hs = plan.hot_stats(reset=True)
+    pcm = d_p.cpu().numpy().view(np.int16).reshape(n, 576, 2)
+    plan.execute(d_g, d_c, d_p, stream=torch.cuda.current_stream().cuda_stream)
+    again = plan.hot_stats()
+    plan.close()
+    assert_close(pcm, want, f"loud {frac}")
+    assert again == hs  # reset, then the same launch counts the same
+    # every granule hot by the reference-order hybrid output gets its PCM
+    # rewritten, and its zone reaches two granules on (frame.go:473-476,
+    # :637-652); the pass also re-tests its replays, counted in "hot" too
+    ref = int(hot_ref.sum())
+    assert 0.8 * ref <= hs["rewritten"] <= 3 * ref + 16, (hs, ref)
+    assert hs["run"] >= hs["rewritten"] and hs["hot"] >= 0.8 * ref, (hs, ref)
+    assert 0.005 < ref / n < 0.25, ref

@@ -40,8 +40,8 @@ fi
 cfgs="c2 c3"; [ "$WHICH" != both ] && cfgs=$WHICH
 for cfg in $cfgs; do
   steps=20; [ $cfg = c3 ] && steps=5
-  H="bench.py --config $cfg --steps 20 --warmup 10 --single-mode --no-cpu-baseline --no-bitstream --no-polyphase --no-c2 --no-pipelined $EXTRA"
-  B="bench.py --config $cfg --steps $steps --warmup 10 --no-cpu-baseline --no-pipelined --no-c2 $EXTRA"
+  H="bench.py --config $cfg --steps 20 --warmup 10 --single-mode --no-cpu-baseline --no-bitstream --no-polyphase --no-c2 --no-pipelined --no-hot $EXTRA"
+  B="bench.py --config $cfg --steps $steps --warmup 10 --no-cpu-baseline --no-pipelined --no-c2 --no-hot $EXTRA"
   run head_$cfg 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_${TAG}_${cfg}_head -o run -- python3 $H
   run trace_$cfg 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_${TAG}_${cfg}_trace -o run -- python3 $B
   run fetch_$cfg 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/prof_${TAG}_${cfg}_fetch -o run -- python3 $B
