@@ -338,10 +338,12 @@ def hot_leg(args, rank, dev, stream, g, c, streams, local, d_c, fracs=(0.006, 0.
         e1.record(stream)
         torch.cuda.synchronize(dev)
         ms = e0.elapsed_time(e1) / args.steps
-        plan.hot_stats(reset=True)
-        plan.execute(d_g2, d_c, d_p, stream=h)
-        hs = plan.hot_stats()
         plan.close()
+        # the counting build of the kernel (MP3G_FLAG_HOT_STATS), one launch
+        cplan = mp3g.Plan(streams, mode=mp3g.MODE_FAST | mp3g.FLAG_HOT_STATS, device=local)
+        cplan.execute(d_g2, d_c, d_p, stream=h)
+        hs = cplan.hot_stats()
+        cplan.close()
         r = {"loud_granules": round(float(mask.mean()), 5), "hot_fraction": round(hs["hot"] / n, 5),
              "rerun_fraction": round(hs["run"] / n, 5), "rewritten_fraction": round(hs["rewritten"] / n, 5),
              "kernel_ms": round(ms, 4), "frames_per_s": round(n / 2 / (ms * 1e-3), 1)}
@@ -723,16 +725,18 @@ def main():
     # the fast kernel's hot-granule fallback on the timed input itself: one
     # more launch with the plan's counters
     hot_timed = None
-    if "fast" in res:
-        hp_ = mp3g.Plan(streams, granules_per_chunk=args.chunk, mode=mp3g.MODE_FAST, device=local)
+    if "fast" in res and hasattr(mp3g.lib(), "mp3g_plan_hot_stats"):
+        hp_ = mp3g.Plan(streams, granules_per_chunk=args.chunk, mode=mp3g.MODE_FAST | mp3g.FLAG_HOT_STATS,
+                        device=local)
         hp_.execute(d_g, d_c, d_pcm, stream=h)
         hs = hp_.hot_stats()
         hp_.close()
         hot_timed = {"hot_fraction": round(hs["hot"] / n_gran, 6), "rerun_fraction": round(hs["run"] / n_gran, 6),
                      "rewritten_fraction": round(hs["rewritten"] / n_gran, 6),
-                     "counts": hs, "source": "mp3g_plan_hot_stats after one launch of the timed input"}
+                     "counts": hs, "source": "mp3g_plan_hot_stats after one launch of the timed input "
+                                             "(the counting build, MP3G_FLAG_HOT_STATS)"}
     hot_cliff = None
-    if args.config == "c3" and not args.no_hot and "fast" in res:
+    if args.config == "c3" and not args.no_hot and hot_timed is not None:
         hot_cliff = hot_leg(args, rank, dev, stream, g, c, streams, local, d_c)
 
     bitstream = None

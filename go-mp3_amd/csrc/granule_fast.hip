@@ -1001,7 +1001,10 @@ __device__ __forceinline__ void record_hot(Smem& s, uint32_t& nz, const mp3g_gra
 // kStamp: diagnostic build -- per-phase s_memtime cycle sums of every wave go
 // to `stamps` (kPhases per workgroup); never used for output.
 constexpr int kPhases = 8;
-template <bool kStamp>
+// kHotCount: the build of MP3G_FLAG_HOT_STATS plans -- the hot-zone pass adds
+// its work to hot_count (kHotCounters); a separate instantiation because the
+// counting alone cost the production kernel ~1.5 % (register allocation).
+template <bool kStamp, bool kHotCount = false>
 __global__ void __launch_bounds__(kLanes * kWaves, MP3G_FAST_WAVES_PER_SIMD)
 granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, const mp3g_granule* __restrict__ gran,
                     const int16_t* __restrict__ coef, const mp3g_state* __restrict__ state_in,
@@ -1673,7 +1676,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     }
     if (done >= end) export_state(zst);
     // (rare: one vector atomic per counter from lane 0 of a chunk with zones)
-    if (hot_count && lane_fresh() == 0) {
+    if (kHotCount && lane_fresh() == 0) {
       atomicAdd(hot_count + 0, n_out);
       atomicAdd(hot_count + 1, n_run);
       atomicAdd(hot_count + 2, n_hot);

@@ -589,8 +589,21 @@ struct mp3g_decoder {
   // The read-ahead has parsed further; a seek that reads nothing (to or past
   // the end, decode.go:110-113) must leave the source there, so that the next
   // Read decodes the frame the reference decodes.
-  void rewind_read_ahead() {
-    if (next_end < frame_src_ends.size()) src.seek(frame_src_ends[next_end], 0, nullptr);
+  // false: the source's Seek failed (the reader's error is then pending in
+  // src.read_failed, for seek_status)
+  bool rewind_read_ahead() {
+    return next_end >= frame_src_ends.size() || src.seek(frame_src_ends[next_end], 0, nullptr);
+  }
+
+  // The status of a failed source Seek: the Seeker's own error in reader mode
+  // (decode.go:164-214 and :128-133 return it), MP3G_ERR_PARSE over bytes
+  // (a bytes.Reader fails only on a negative position).
+  int seek_status(const char* what) {
+    if (src.rd) {
+      src.read_failed = true;
+      return read_status(St::kErr);
+    }
+    return abi_fail(MP3G_ERR_PARSE, what);
   }
 
   // readFrame for Read: serve the next batch (read-ahead grows to
@@ -665,8 +678,8 @@ struct mp3g_decoder {
   int ensure_length() {
     if (length != -1 || !src.seekable) return MP3G_OK;
     int64_t keep = 0;
-    src.seek(0, 1, &keep);
-    src.seek(0, 0, nullptr);  // rewind
+    if (!src.seek(0, 1, &keep)) return seek_status("seek");
+    if (!src.seek(0, 0, nullptr)) return seek_status("rewind");
     src.pos = 0;
     St st = src.skip_tags();
     if (st != St::kOk) return read_status(st);
@@ -681,10 +694,10 @@ struct mp3g_decoder {
       frame_starts.push_back(p);
       bytes_per_frame = host::header_bytes_per_frame(h);
       l += bytes_per_frame;
-      src.seek(host::header_frame_size(h) - 4, 1, nullptr);
+      if (!src.seek(host::header_frame_size(h) - 4, 1, nullptr)) return seek_status("seek");
     }
     length = l;
-    src.seek(keep, 0, nullptr);
+    if (!src.seek(keep, 0, nullptr)) return seek_status("seek");
     return MP3G_OK;
   }
 };
@@ -883,7 +896,7 @@ int mp3g_decoder_seek(mp3g_decoder* d, int64_t offset, int whence, int64_t* newp
   }
   d->pos = npos;
   d->cancel_read_ahead();
-  d->rewind_read_ahead();
+  if (!d->rewind_read_ahead()) return d->seek_status("seek");
   d->buf_reset();
   d->reset_reservoir();  // d.frame = nil
   d->md.clear();
@@ -904,7 +917,7 @@ int mp3g_decoder_seek(mp3g_decoder* d, int64_t offset, int whence, int64_t* newp
   if (f > 0) f--;
   if (f >= (int64_t)d->frame_starts.size())
     return abi_fail(MP3G_ERR_UNSUPPORTED, "frame index out of range (the reference panics)");
-  if (!d->src.seek(d->frame_starts[f], 0, nullptr)) return abi_fail(MP3G_ERR_PARSE, "seek");
+  if (!d->src.seek(d->frame_starts[f], 0, nullptr)) return d->seek_status("seek");
   int rc = d->refill();
   if (rc != MP3G_OK) return rc;
   if ((int)d->frame_ends.size() < need) {  // the reference's 2nd readFrame failed

@@ -52,10 +52,13 @@ hipError_t launch_fast(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_
   const dim3 grid((n_chunks + v3::kWaves - 1) / v3::kWaves), block(64 * v3::kWaves);
   if (d_stamps)
     hipLaunchKernelGGL(v3::granule_fast_kernel<true>, grid, block, 0, stream, d_chunks, n_chunks, d_gran, d_coef,
-                       d_state_in, d_state_out, d_pcm, d_stamps, d_hot);
+                       d_state_in, d_state_out, d_pcm, d_stamps, nullptr);
+  else if (d_hot)
+    hipLaunchKernelGGL((v3::granule_fast_kernel<false, true>), grid, block, 0, stream, d_chunks, n_chunks, d_gran,
+                       d_coef, d_state_in, d_state_out, d_pcm, nullptr, d_hot);
   else
     hipLaunchKernelGGL(v3::granule_fast_kernel<false>, grid, block, 0, stream, d_chunks, n_chunks, d_gran, d_coef,
-                       d_state_in, d_state_out, d_pcm, nullptr, d_hot);
+                       d_state_in, d_state_out, d_pcm, nullptr, nullptr);
   return hipGetLastError();
 }
 

@@ -415,7 +415,7 @@ int mp3g_plan_execute(mp3g_plan* p, const mp3g_granule* d_gran, const int16_t* d
     if ((c.flags & kChunkStateOut) && !d_state_out) return fail(MP3G_ERR_INVALID_ARGUMENT, "state_out needed");
   }
   return plan_launch(p->mode, p->d_chunks, (uint32_t)p->chunks.size(), d_gran, d_coef, d_state_in, d_state_out, d_pcm,
-                     p->d_hot, static_cast<hipStream_t>(hip_stream));
+                     (p->mode & MP3G_FLAG_HOT_STATS) ? p->d_hot : nullptr, static_cast<hipStream_t>(hip_stream));
 }
 
 // The fast kernel's hot-granule counters of this plan, summed over its

@@ -14,7 +14,7 @@ import time
 import numpy as np
 
 __all__ = ["CHANNEL_DTYPE", "GRANULE_DTYPE", "STREAM_DTYPE", "STATE_DTYPE", "MODE_EXACT",
-           "MODE_FAST", "FLAG_CHECKED", "FLAG_KERNEL_V1", "FLAG_KERNEL_V2", "FLAG_HOST_HUFFMAN", "STATE_IN", "STATE_OUT", "Mp3gError", "lib", "lib_path",
+           "MODE_FAST", "FLAG_CHECKED", "FLAG_KERNEL_V1", "FLAG_KERNEL_V2", "FLAG_HOT_STATS", "FLAG_HOST_HUFFMAN", "STATE_IN", "STATE_OUT", "Mp3gError", "lib", "lib_path",
            "decode_host", "validate", "Plan", "device_count", "streams_for", "parse_stream",
            "parse_streams", "Decoder", "HJOB_DTYPE", "scan_streams", "huffman_execute", "HUFF_ROWS_COUNT1",
            "HUFF_STAGE_WIDE", "HUFF_STAGE_MID", "huffman_stage_flags", "decode_streams"]
@@ -41,6 +41,7 @@ assert STREAM_DTYPE.itemsize == 16 and STATE_DTYPE.itemsize == 12800
 
 MODE_EXACT, MODE_FAST, FLAG_CHECKED, FLAG_KERNEL_V1, FLAG_HOST_HUFFMAN = 0, 1, 0x100, 0x200, 0x400
 FLAG_KERNEL_V2 = 0x800  # exact mode via the workgroup v2 kernel (cross-check of the default v4)
+FLAG_HOT_STATS = 0x1000  # fast plans: count the hot-granule fallback's work (Plan.hot_stats)
 STATE_IN, STATE_OUT = 1, 2
 MP3G_PCM_BYTES_PER_GRANULE = 2304  # include/mp3g.h: 576 stereo s16 samples
 
@@ -92,7 +93,8 @@ def lib():
         L.mp3g_plan_info.argtypes = [vp, C.POINTER(u64), C.POINTER(u64), C.POINTER(u64)]
         L.mp3g_plan_execute.argtypes = [vp, vp, vp, vp, vp, vp, vp]
         L.mp3g_plan_synth_execute.argtypes = [vp, vp, vp, vp, vp, vp, vp]
-        L.mp3g_plan_hot_stats.argtypes = [vp, C.POINTER(u64), C.c_int]
+        if hasattr(L, "mp3g_plan_hot_stats"):  # ABI 5 (an older build through MP3G_LIB: A/B runs)
+            L.mp3g_plan_hot_stats.argtypes = [vp, C.POINTER(u64), C.c_int]
         L.mp3g_decode_host.argtypes = [C.c_int, vp, vp, u64, vp, u32, vp, vp, vp, u32]
         L.mp3g_plan_debug_phases.argtypes = [vp, vp, vp, vp, C.POINTER(u64), vp]
         L.mp3g_plan_debug_timeline.argtypes = [vp, vp, vp, vp, C.POINTER(u64), vp]
@@ -474,20 +476,27 @@ class Decoder:
         self.read_errors = []
 
         def _read(_user, buf, cap):
+            # (everything inside the try: an exception escaping a ctypes
+            # callback would return 0, a silent EOF)
             try:
                 b = read(int(cap))
+                if not isinstance(b, (bytes, bytearray, memoryview)):
+                    raise TypeError(f"read() returned {type(b).__name__}, not bytes")
+                if len(b) > int(cap):
+                    raise ValueError(f"read({int(cap)}) returned {len(b)} bytes")
+                k = len(b)
+                if k:
+                    C.memmove(buf, bytes(b), k)
+                return k
             except Exception as e:  # a reader error: the decoder returns MP3G_ERR_READ
                 self.read_errors.append(e)
                 return -1
-            k = min(len(b), int(cap))
-            if k:
-                C.memmove(buf, b, k)
-            return k
 
         def _seek(_user, off, whence):
             try:
                 return int(seek(int(off), int(whence)))
-            except Exception:
+            except Exception as e:  # the Seeker's error: MP3G_ERR_READ
+                self.read_errors.append(e)
                 return -1
 
         # the callbacks must outlive the decoder
@@ -602,8 +611,9 @@ class Plan:
                                              C.c_void_p(stream) if stream else None))
 
     def hot_stats(self, reset=False):
-        """Fast plans: the hot-granule fallback's work summed over this plan's
-        launches (mp3g_plan_hot_stats, synchronous): granules whose PCM the
+        """Fast plans created with FLAG_HOT_STATS: the hot-granule fallback's
+        work summed over this plan's launches (mp3g_plan_hot_stats,
+        synchronous): granules whose PCM the
         reference-order pass rewrote, granules it ran (with the replays of
         their entry state), hot granules it met."""
         out = (C.c_uint64 * 3)()

@@ -117,8 +117,11 @@ def gather_pcm(pcm, dst=0, out=None):
     import torch
     import torch.distributed as dist
     world, rank = dist.get_world_size(), dist.get_rank()
+    if rank == dst and out is not None and not out.is_contiguous():
+        # (reshape would receive into a copy and leave `out` unfilled)
+        raise ValueError("gather_pcm: out must be contiguous")
     dtype = pcm.dtype
-    flat = pcm.reshape(-1).view(torch.uint8)  # neither gloo nor RCCL has an int16 type
+    flat = pcm.contiguous().reshape(-1).view(torch.uint8)  # neither gloo nor RCCL has an int16 type
     n = torch.tensor([flat.numel()], dtype=torch.int64, device=flat.device)
     sizes = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(sizes, n)

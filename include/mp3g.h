@@ -38,7 +38,8 @@ extern "C" {
  * 4: main-data kernel stages for high bitrates -- MP3G_HUFF_STAGE_MID /
  *    MP3G_HUFF_STAGE_WIDE flags of mp3g_huffman_execute_ex and the advice
  *    mp3g_huffman_stage_flags.
- * 5: mp3g_plan_hot_stats (the fast kernel's hot-granule fallback counters). */
+ * 5: mp3g_plan_hot_stats and MP3G_FLAG_HOT_STATS (the fast kernel's
+ *    hot-granule fallback counters). */
 #define MP3G_ABI_VERSION 5
 
 /* ---- status codes ------------------------------------------------------ */
@@ -142,6 +143,8 @@ typedef struct mp3g_stream {
                                       default exact kernel is v4, one wave per chunk) */
 #define MP3G_FLAG_HOST_HUFFMAN 0x400u /* decoder: scale factors + Huffman on the host (mp3g_parse_*)
                                          instead of the GPU main-data kernel (cross-check) */
+#define MP3G_FLAG_HOT_STATS 0x1000u /* fast-mode plans: count the hot-granule fallback's work
+                                       (mp3g_plan_hot_stats; a kernel build that costs ~1.5 %) */
 
 /* ---- library / device ---------------------------------------------------- */
 int mp3g_abi_version(void);
@@ -200,11 +203,12 @@ int mp3g_plan_synth_execute(mp3g_plan* plan, const mp3g_granule* d_granules,
 /* Fast-mode plans: the work of the hot-granule fallback (granules whose
  * hybrid output exceeds the fast transforms' magnitude bound run again in the
  * reference's operation order), summed over the plan's
- * launches since creation or the last reset.  out3[0]: granules whose PCM that
+ * launches since creation or the last reset, for plans created with
+ * MP3G_FLAG_HOT_STATS (others: always 0).  out3[0]: granules whose PCM that
  * pass rewrote; out3[1]: granules it ran, the replays of their entry state
  * included; out3[2]: hot granules it met.  Synchronises the device; reset != 0
- * zeroes the counters after reading.  (Exact-mode plans: always 0.)  No
- * reference counterpart: go-mp3 has one arithmetic (frame.go:140-688). */
+ * zeroes the counters after reading.  No reference counterpart: go-mp3 has one
+ * arithmetic (frame.go:140-688). */
 int mp3g_plan_hot_stats(mp3g_plan* plan, uint64_t* out3, int reset);
 
 /* ---- synchronous host-buffer decode (the cgo drop-in entry) --------------

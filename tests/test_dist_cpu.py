@@ -131,3 +131,24 @@ def test_shard_frames_partition_and_oracle_exact():
             pcm, _ = oracle.dsp_streams(g[h:hi], c[h:hi], mp3g.streams_for([hi - h]))
             got.append(pcm[lo - h:])
         assert np.array_equal(np.concatenate(got), want), f"world {world}"
+
+
+def test_gather_rejects_noncontiguous_out():
+    """A non-contiguous `out` would be received into a reshape copy and left
+    unfilled: gather_pcm refuses it.  One gloo rank, so the
+    refusal cannot leave a peer waiting."""
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        pcm = torch.arange(64, dtype=torch.int16)
+        with pytest.raises(ValueError, match="contiguous"):
+            mdist.gather_pcm(pcm, out=torch.zeros((64, 2), dtype=torch.int16)[:, 0])
+        out = torch.zeros(64, dtype=torch.int16)
+        assert mdist.gather_pcm(pcm[::1], out=out) is out and torch.equal(out, pcm)
+        # a non-contiguous source is gathered as its values
+        src = torch.arange(128, dtype=torch.int16)[::2]
+        assert torch.equal(mdist.gather_pcm(src), src)
+    finally:
+        dist.destroy_process_group()

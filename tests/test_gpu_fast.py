@@ -315,7 +315,7 @@ def test_fast_loud_batch_and_hot_counters(gpu, frac):
     d_g = torch.from_numpy(g.view(np.uint8).copy()).cuda()
     d_c = torch.from_numpy(c.view(np.uint8).reshape(-1).copy()).cuda()
     d_p = torch.zeros(n * 2304, dtype=torch.uint8, device="cuda")
-    plan = gpu.Plan(s, mode=gpu.MODE_FAST)
+    plan = gpu.Plan(s, mode=gpu.MODE_FAST | gpu.FLAG_HOT_STATS)
     assert plan.hot_stats() == {"rewritten": 0, "run": 0, "hot": 0}
     plan.execute(d_g, d_c, d_p, stream=torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
@@ -326,6 +326,14 @@ def test_fast_loud_batch_and_hot_counters(gpu, frac):
     plan.close()
     assert_close(pcm, want, f"loud {frac}")
     assert again == hs  # reset, then the same launch counts the same
+    # the production build (no MP3G_FLAG_HOT_STATS) decodes the same PCM and counts nothing
+    plain = gpu.Plan(s, mode=gpu.MODE_FAST)
+    d_p.zero_()
+    plain.execute(d_g, d_c, d_p, stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert plain.hot_stats() == {"rewritten": 0, "run": 0, "hot": 0}
+    plain.close()
+    assert np.array_equal(d_p.cpu().numpy().view(np.int16).reshape(n, 576, 2), pcm)
     # every granule hot by the reference-order hybrid output gets its PCM
     # rewritten, and its zone reaches two granules on (frame.go:473-476,
     # :637-652); the pass also re-tests its replays, counted in "hot" too

@@ -220,3 +220,44 @@ def test_stream_reader_error(gpu, sample_files):
     with pytest.raises(gpu.Mp3gError) as e:  # failing before frame 0: NewDecoder fails with it
         gpu.Decoder.from_reader(PieceReader(data, 1, fail_at=100).read, None)
     assert e.value.status == gpu.ERR_READ
+
+
+def test_stream_seek_error(gpu, sample_files):
+    """A Seeker that fails: NewDecoder's frame-start walk
+    (ensureFrameStartsAndLength, decode.go:164-214) returns the Seeker's error
+    instead of walking from the wrong offset; a Seek whose source seek fails
+    returns it too (decode.go:128-133)."""
+    data = sample_files["classic_lame.mp3"]
+
+    def bad_seek(off, whence):
+        raise IOError("seek failed")
+
+    with pytest.raises(gpu.Mp3gError) as e:  # the walk's first Seek
+        gpu.Decoder.from_reader(PieceReader(data, 5).read, bad_seek)
+    assert e.value.status == gpu.ERR_READ
+    # seeks that work until NewDecoder returned, then fail
+    r = PieceReader(data, 6)
+    state = {"ok": True}
+
+    def seek_until(off, whence):
+        if not state["ok"]:
+            raise IOError("seek failed later")
+        return r.seek(off, whence)
+
+    d = gpu.Decoder.from_reader(r.read, seek_until)
+    st, b = d.read(4608)
+    assert st == 0 and len(b) == 4608
+    state["ok"] = False
+    st, _ = d.seek(100 * 4608, 0)
+    assert st == gpu.ERR_READ and any("later" in str(x) for x in d.read_errors)
+    d.close()
+
+
+def test_stream_reader_bad_values(gpu, sample_files):
+    """read() returning a non-bytes value or more than asked is a reader error
+    (MP3G_ERR_READ), not a silent EOF or a truncated piece."""
+    data = sample_files["classic_lame.mp3"]
+    for bad in (lambda n: None, lambda n: b"\0" * (n + 1)):
+        with pytest.raises(gpu.Mp3gError) as e:
+            gpu.Decoder.from_reader(bad, None)
+        assert e.value.status == gpu.ERR_READ
