@@ -273,6 +273,10 @@ def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle, pip
            "huffman_algorithmic_bytes_per_launch": md + n * (96 + 126) + coef_bytes,
            "huffman_algorithmic_gbps": round((md + n * (96 + 126) + coef_bytes) / (huff_ms * 1e-3) / 1e9, 2),
            "huffman_traffic_bytes_per_launch": profiled_traffic(cfg, "mp3g::huff::huffman_sorted_kernel")[0],
+           # WRITE_SIZE reads this kernel's 32-B row blocks (written between
+           # symbol decodes, so a row's 128-B line is evicted half-written)
+           # at 1.61x their bytes: tools/store_calib.hip
+           "huffman_write_size_calibration": huffman_write_calibration(),
            "main_data_bytes": md, "bitstream_bytes": int(sum(len(d) for d in datas)),
            "host_scan_s": round(scan_s, 4), "host_scan_frames_per_s": round(frames / scan_s, 1),
            "host_scan_threads": 16, "writer_s": round(writer_s, 2),
@@ -345,8 +349,10 @@ def hot_leg(args, rank, dev, stream, g, c, streams, local, d_c, fracs=(0.006, 0.
         hs = cplan.hot_stats()
         cplan.close()
         r = {"loud_granules": round(float(mask.mean()), 5), "hot_fraction": round(hs["hot"] / n, 5),
-             "rerun_fraction": round(hs["run"] / n, 5), "rewritten_fraction": round(hs["rewritten"] / n, 5),
-             "kernel_ms": round(ms, 4), "frames_per_s": round(n / 2 / (ms * 1e-3), 1)}
+             "rewritten_fraction": round(hs["rewritten"] / n, 5), "zones": hs["zones"],
+             "in_wave_rerun_fraction": round(hs["in_wave"] / n, 5),
+             "kernel_ms": round(ms, 4), "frames_per_s": round(n / 2 / (ms * 1e-3), 1),
+             "timing": "fast kernel + zone launch (exact v4 over the deferred zones), HIP events"}
         if rank == 0 and not args.no_cpu_baseline and frac == fracs[-1]:
             sys.path.insert(0, os.path.join(REPO, "oracle"))
             import oracle  # checker of the timed output only
@@ -358,6 +364,18 @@ def hot_leg(args, rank, dev, stream, g, c, streams, local, d_c, fracs=(0.006, 0.
         out.append(r)
         del d_g2
     return out
+
+
+def huffman_write_calibration():
+    """WRITE_SIZE / known bytes of the main-data kernel's store pattern (a
+    32-B row writer with a decode between blocks) from the kept calibration."""
+    f = os.path.join(REPO, "profiles", "r05_store_calib.json")
+    try:
+        rows = {r["kernel"]: r for r in json.load(open(f))["rows"]}
+        return {"factor": rows["k_slow32"]["ratio"], "streaming_16B": rows["k_stream16"]["ratio"],
+                "source": os.path.relpath(f, REPO)}
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 POLY_BYTES_PER_GC = 576 * 4 + 576 * 2  # SURVEY.md 8(d): f32 lines in + s16 PCM out per granule-channel
@@ -731,7 +749,7 @@ def main():
         hp_.execute(d_g, d_c, d_pcm, stream=h)
         hs = hp_.hot_stats()
         hp_.close()
-        hot_timed = {"hot_fraction": round(hs["hot"] / n_gran, 6), "rerun_fraction": round(hs["run"] / n_gran, 6),
+        hot_timed = {"hot_fraction": round(hs["hot"] / n_gran, 6), "zones": hs["zones"],
                      "rewritten_fraction": round(hs["rewritten"] / n_gran, 6),
                      "counts": hs, "source": "mp3g_plan_hot_stats after one launch of the timed input "
                                              "(the counting build, MP3G_FLAG_HOT_STATS)"}

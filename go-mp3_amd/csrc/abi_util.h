@@ -23,7 +23,8 @@ int ensure_device_ready(int device);
 // (mp3g_decode_streams_into) instead of through a plan's blocking copy.
 int plan_chunks(int device, const mp3g_stream* streams, uint32_t n_streams, uint32_t granules_per_chunk,
                 uint32_t mode, std::vector<ChunkDesc>* chunks, uint64_t* n_granules, uint64_t* n_halo);
+struct ZoneScratch;  // kernels.h
 int plan_launch(uint32_t mode, const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_granule* d_gran,
                 const int16_t* d_coef, const mp3g_state* d_state_in, mp3g_state* d_state_out, int16_t* d_pcm,
-                uint32_t* d_hot, hipStream_t stream);
+                uint32_t* d_hot, const ZoneScratch* zones, hipStream_t stream);
 }  // namespace mp3g

@@ -965,24 +965,20 @@ __device__ __forceinline__ uint32_t zone_end(const mp3g_granule* __restrict__ gr
 }
 
 // Zones recorded by the fast pass (WaveSmem::zone): a hot granule g opens
-// (or extends) the zone [max(g, out_first), g + 2) of granules whose PCM
-// depends on its hybrid output; the zone pass, which re-detects g as hot in
-// the reference's arithmetic, extends it to zone_end(g) (kept out of the
-// granule loop: its register budget).  (If the exact S of g is not hot, the
-// fast V of g is within the fast bound and nothing past g + 2 needs redoing.)
-// A replayed granule g < out_first whose V reaches an output only across a
-// mono run gets its zone_end here.  When the list is full the last zone runs
-// to the chunk end.
+// (or extends) the zone [max(g, out_first), zone_end(g)) of granules whose
+// PCM depends on its hybrid output (a replayed granule g < out_first whose V
+// reaches an output only across a mono run included); the in-wave zone pass
+// also extends a zone when its exact arithmetic meets a hot granule.  When
+// the list is full the last zone runs to the chunk end.
 template <class Smem>
 __device__ __forceinline__ void record_hot(Smem& s, uint32_t& nz, const mp3g_granule* __restrict__ gran, uint32_t g,
                                            uint32_t out_first, uint32_t end) {
   // (wave-uniform throughout: every lane stores the same values)
+  // (zone_end here, not only in the in-wave pass: a zone deferred to the zone
+  // list gets no exact re-detection to extend it across a mono run)
   const uint32_t zs = g > out_first ? g : out_first;
-  uint32_t ze = g + 2 < end ? g + 2 : end;
-  if (zs >= ze) {
-    ze = zone_end(gran, g, end);
-    if (zs >= ze) return;  // a replayed granule whose V no output reads
-  }
+  const uint32_t ze = zone_end(gran, g, end);
+  if (zs >= ze) return;  // a replayed granule whose V no output reads
   const uint32_t last_end = nz ? __builtin_amdgcn_readfirstlane(s.zone[nz - 1][1]) : 0u;
   if (nz > 0 && zs <= last_end) {
     s.zone[nz - 1][1] = ze > last_end ? ze : last_end;
@@ -1009,7 +1005,8 @@ __global__ void __launch_bounds__(kLanes * kWaves, MP3G_FAST_WAVES_PER_SIMD)
 granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, const mp3g_granule* __restrict__ gran,
                     const int16_t* __restrict__ coef, const mp3g_state* __restrict__ state_in,
                     mp3g_state* __restrict__ state_out, int16_t* __restrict__ pcm,
-                    unsigned long long* __restrict__ stamps, uint32_t* __restrict__ hot_count) {
+                    unsigned long long* __restrict__ stamps, uint32_t* __restrict__ hot_count,
+                    ChunkDesc* __restrict__ zone_list, uint32_t* __restrict__ zone_count, uint32_t zone_cap) {
   unsigned long long ph[kPhases] = {}, tprev = 0, rt[4] = {};
   if constexpr (kStamp) rt[0] = __builtin_amdgcn_s_memrealtime();
   auto stamp = [&](int p) {
@@ -1185,6 +1182,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
   // takes a higher priority, which keeps the co-resident waves abreast.
   const uint32_t span = end - w, span2 = 2 * span, span3 = 3 * span;
   uint32_t nz = 0;  // hot zones recorded (s.zone)
+  uint32_t n_flagged = 0;  // hot granules the pass flagged (kHotCount builds)
   for (uint32_t g = w; g < end; g++) {
     if (MP3G_FAST_PRIO) {
       const uint32_t left4 = 4u * (end - g);  // priority floor(4 * left / span), 3 .. 0
@@ -1564,7 +1562,10 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     // the second test (rare) on S in the ring: the granule's zone is redone
     // in the reference's order after the pass (a granule whose V feeds no
     // output needs no zone)
-    if (hot1 && need_v && slot_sums_hot(s.ring, nch)) record_hot(s, nz, gran, g, out_first, end);
+    if (hot1 && need_v && slot_sums_hot(s.ring, nch)) {
+      record_hot(s, nz, gran, g, out_first, end);
+      if constexpr (kHotCount) n_flagged++;
+    }
 #endif
     stamp(4);
     {
@@ -1641,11 +1642,55 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
   //      granule's hybrid output.  A zone reaching the chunk end also rewrites
   //      the exported state.  (The zones' stages mirror the fast loop's, in
   //      the reference's operation order: exact_granule.) ----
-  if (nz) {
+  // ---- hot zones (rare), deferred: appended to the launch's zone list as
+  //      chunks of their own, which the exact v4 kernel then decodes in the
+  //      reference's order over many waves (launch_fast: the zone launch).
+  //      The in-wave pass below is the fallback when the list is full (and
+  //      the path of the diagnostic builds, which pass no list). ----
+  bool in_wave = nz != 0;
+  if (nz && zone_list) {
+    uint32_t base = 0;
+    if (lane_fresh() == 0) base = atomicAdd(zone_count, nz);
+    base = __builtin_amdgcn_readfirstlane(base);  // lane 0 is the first active lane
+    const int zl = lane_fresh();
+    if (base + nz <= zone_cap) {
+      in_wave = false;
+      if ((uint32_t)zl < nz) {
+        const uint32_t zs = s.zone[zl][0], ze = s.zone[zl][1];
+        ChunkDesc z;
+        z.out_first = zs;
+        z.stream_first = cd.stream_first;
+        z.n_out = ze - zs;
+        z.stream = cd.stream;
+        // entry state as the chunk's; the exported state when the zone ends
+        // the chunk (it then overwrites this pass's export)
+        z.flags = (cd.flags & kChunkStateIn) | (ze == end ? (cd.flags & kChunkStateOut) : 0u);
+        z.reserved = 0;
+        zone_list[base + zl] = z;
+      }
+      if constexpr (kHotCount) {
+        uint32_t n_out = 0;
+        for (uint32_t i = 0; i < nz; i++)
+          n_out += __builtin_amdgcn_readfirstlane(s.zone[i][1]) - __builtin_amdgcn_readfirstlane(s.zone[i][0]);
+        if (lane_fresh() == 0) {
+          atomicAdd(hot_count + 0, n_out);
+          atomicAdd(hot_count + 1, nz);
+          atomicAdd(hot_count + 2, n_flagged);
+        }
+      }
+    } else if (base + (uint32_t)zl < zone_cap && (uint32_t)zl < nz) {
+      // the slots this wave took below the capacity hold no zone
+      ChunkDesc z = {};
+      z.out_first = cd.out_first;
+      z.stream_first = cd.stream_first;
+      zone_list[base + zl] = z;
+    }
+  }
+  if (in_wave) {
     f2 zst[9];  // the zones' own overlap state (nothing flows in from the fast pass)
     uint32_t done = 0;  // the exact state in zst / the ring is valid for granules < done
     bool have = false;
-    uint32_t n_out = 0, n_run = 0, n_hot = 0;  // for hot_count (kernels.h kHotCounters)
+    uint32_t n_out = 0, n_run = 0;  // for hot_count (kernels.h kHotCounters)
     for (uint32_t i = 0; i < nz; i++) {
       const uint32_t zs = __builtin_amdgcn_readfirstlane(s.zone[i][0]);
       uint32_t ze = __builtin_amdgcn_readfirstlane(s.zone[i][1]);
@@ -1669,7 +1714,6 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
         if (exact_granule(gran, coef, pcm, s, sh, gz, gz >= zs, nv, zst)) {
           const uint32_t e = zone_end(gran, gz, end);
           ze = e > ze ? e : ze;
-          n_hot++;
         }
       }
       done = gz;
@@ -1678,8 +1722,9 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     // (rare: one vector atomic per counter from lane 0 of a chunk with zones)
     if (kHotCount && lane_fresh() == 0) {
       atomicAdd(hot_count + 0, n_out);
-      atomicAdd(hot_count + 1, n_run);
-      atomicAdd(hot_count + 2, n_hot);
+      atomicAdd(hot_count + 1, nz);
+      atomicAdd(hot_count + 2, n_flagged);
+      atomicAdd(hot_count + 3, n_run);
     }
   }
   if constexpr (kStamp) {

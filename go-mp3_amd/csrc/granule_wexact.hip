@@ -216,13 +216,37 @@ __device__ __forceinline__ void init_state_exact(XWaveSmem& s, const mp3g_state*
 
 }  // namespace
 
+__device__ __forceinline__ void wexact_chunk(const ChunkDesc& cd, const mp3g_granule* __restrict__ gran,
+                                             const int16_t* __restrict__ coef, const mp3g_state* __restrict__ state_in,
+                                             mp3g_state* __restrict__ state_out, int16_t* __restrict__ pcm,
+                                             XWaveSmem& s, const XSharedSmem& sh);
+
+// kZones: the zone launch of a fast-mode plan (kernels_fast.hip launch_fast):
+// `chunks` is the zone list the fast kernel filled -- hot zones as chunks of
+// their own, to be decoded in the reference's order -- with its length in
+// zone_counts[0] (n_chunks = the list's capacity).  The waves take zone after
+// zone; the last workgroup to finish (zone_counts[1] counts them) empties the
+// list for the next launch, after every workgroup has read its length.  An
+// empty list ends every workgroup at once and leaves the counters alone, so
+// the launch pair needs no host-side state (graph replays included).
+template <bool kZones = false>
 __global__ void __launch_bounds__(kLanes * kXWaves, 4)
 granule_wexact_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, const mp3g_granule* __restrict__ gran,
                       const int16_t* __restrict__ coef, const mp3g_state* __restrict__ state_in,
-                      mp3g_state* __restrict__ state_out, int16_t* __restrict__ pcm) {
+                      mp3g_state* __restrict__ state_out, int16_t* __restrict__ pcm,
+                      uint32_t* __restrict__ zone_counts = nullptr) {
   __shared__ XSharedSmem sh;
   __shared__ XWaveSmem wsm[kXWaves];
-  {
+  uint32_t live = n_chunks;
+  bool work = true;
+  if constexpr (kZones) {
+    const uint32_t c = __builtin_amdgcn_readfirstlane(__hip_atomic_load(zone_counts, __ATOMIC_RELAXED,
+                                                                        __HIP_MEMORY_SCOPE_AGENT));
+    if (c == 0) return;  // (grid-uniform)
+    live = c < n_chunks ? c : n_chunks;
+    work = blockIdx.x * kXWaves < live;  // (workgroup-uniform)
+  }
+  if (work) {
     const int t = threadIdx.x;
     for (int e = t; e < 16; e += kLanes * kXWaves) (&sh.isr[0][0])[e] = e < 14 ? (&g_fast.is_ratio[0][0])[e] : 1.0f;
     for (int e = t; e < kCombos * 32; e += kLanes * kXWaves) (&sh.lband[0][0])[e] = (&g_fast.lband[0][0])[e];
@@ -235,12 +259,38 @@ granule_wexact_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, c
     }
     for (int e = t; e < 4 * 36; e += kLanes * kXWaves) (&sh.win[0][0])[e] = (&g_fast.win[0][0])[e];
   }
-  __syncthreads();  // the only workgroup barrier
-  const int lane = threadIdx.x & (kLanes - 1);
-  const uint32_t ci = __builtin_amdgcn_readfirstlane(blockIdx.x * kXWaves + (threadIdx.x >> 6));
-  if (ci >= n_chunks) return;
+  __syncthreads();  // the table fill (the only workgroup barrier of a plan launch)
   XWaveSmem& s = wsm[threadIdx.x >> 6];
-  const ChunkDesc cd = chunks[ci];
+  if constexpr (kZones) {
+    if (work) {
+      for (uint32_t ci = __builtin_amdgcn_readfirstlane(blockIdx.x * kXWaves + (threadIdx.x >> 6)); ci < live;
+           ci += gridDim.x * kXWaves) {
+        const ChunkDesc cd = chunks[ci];
+        wexact_chunk(cd, gran, coef, state_in, state_out, pcm, s, sh);
+      }
+    }
+    __syncthreads();  // the workgroup is done with the list
+    if (threadIdx.x == 0) {
+      const uint32_t done = __hip_atomic_fetch_add(zone_counts + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      if (done == gridDim.x - 1) {  // the last workgroup: every one has read the length
+        __hip_atomic_store(zone_counts, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(zone_counts + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  } else {
+    const uint32_t ci = __builtin_amdgcn_readfirstlane(blockIdx.x * kXWaves + (threadIdx.x >> 6));
+    if (ci >= live) return;
+    const ChunkDesc cd = chunks[ci];
+    wexact_chunk(cd, gran, coef, state_in, state_out, pcm, s, sh);
+  }
+}
+
+// One chunk in the reference's order (one wave).
+__device__ __forceinline__ void wexact_chunk(const ChunkDesc& cd, const mp3g_granule* __restrict__ gran,
+                                             const int16_t* __restrict__ coef, const mp3g_state* __restrict__ state_in,
+                                             mp3g_state* __restrict__ state_out, int16_t* __restrict__ pcm,
+                                             XWaveSmem& s, const XSharedSmem& sh) {
+  const int lane = threadIdx.x & (kLanes - 1);
   const int ch = lane >> 5, k = lane & 31;
 
   uint64_t w64;

@@ -213,6 +213,9 @@ struct DevMem {
 struct PipeBufs {
   Pinned arena[2];
   DevMem d_gran[2], d_jobs[2], d_md[2], d_chunks[2], d_pcm[2], d_coef;
+  // the fast kernel's deferred hot zones (kernels.h ZoneScratch), used by the
+  // launches on `comp` in order
+  DevMem d_zones;
   // the pipeline's streams and per-slot events (created once per device)
   hipStream_t up = nullptr, comp = nullptr, down = nullptr;
   hipEvent_t h2d[2] = {}, kern[2] = {}, d2h[2] = {};
@@ -589,6 +592,13 @@ int mp3g_decode_streams_into(int device, uint32_t n_streams, const uint8_t* cons
     }
     if (rc == MP3G_OK && !B->d_coef.reserve(max_ng * MP3G_COEF_PER_GRANULE * sizeof(int16_t)))
       rc = abi_fail(MP3G_ERR_DEVICE, "decode_streams_into: buffers");
+    const uint32_t zone_cap = (uint32_t)std::max<uint64_t>(64, max_ng);
+    if (rc == MP3G_OK && B->d_zones.bytes < zone_scratch_bytes(zone_cap)) {
+      // a fresh list: both counts zero
+      if (!B->d_zones.reserve(zone_scratch_bytes(zone_cap)) || hipMemset(B->d_zones.p, 0, 32) != hipSuccess)
+        rc = abi_fail(MP3G_ERR_DEVICE, "decode_streams_into: buffers");
+    }
+    const uint32_t zone_cap_all = (uint32_t)std::min<size_t>((B->d_zones.bytes - 32) / sizeof(ChunkDesc), 0xffffffffu);
     trace.mark("buffers");
     hipStream_t up = B->up, comp = B->comp, down = B->down;
     std::vector<ChunkDesc> chunks;
@@ -671,11 +681,13 @@ int mp3g_decode_streams_into(int device, uint32_t n_streams, const uint8_t* cons
                                    static_cast<const uint8_t*>(B->d_md[slot].p),
                                    static_cast<mp3g_granule*>(B->d_gran[slot].p), static_cast<int16_t*>(B->d_coef.p),
                                    (mode_reads_to_count1(mode) ? MP3G_HUFF_ROWS_COUNT1 : 0u) | stage, comp);
-      if (rc == MP3G_OK && !chunks.empty())
+      if (rc == MP3G_OK && !chunks.empty()) {
+        const ZoneScratch zs = zone_scratch_at(B->d_zones.p, zone_cap_all);
         rc = plan_launch(mode, static_cast<const ChunkDesc*>(B->d_chunks[slot].p), (uint32_t)chunks.size(),
                          static_cast<const mp3g_granule*>(B->d_gran[slot].p),
                          static_cast<const int16_t*>(B->d_coef.p), nullptr, nullptr,
-                         static_cast<int16_t*>(B->d_pcm[slot].p), nullptr, comp);
+                         static_cast<int16_t*>(B->d_pcm[slot].p), nullptr, &zs, comp);
+      }
       if (rc) break;
       e = hipEventRecord(B->kern[slot], comp);
       // down

@@ -312,7 +312,11 @@ MP3G_HD_INLINE int decode_job(const mp3g_hjob& job, uint64_t j, const uint64_t* 
   // the job in the compiler's eyes, which would re-load its fields from memory
   // (with a full vmcnt wait) in every loop iteration
   const mp3g_hjob J = job;
+#ifdef MP3G_HUFF_SINK_ROWS  // timing experiments only: every row into one of 64 L2-resident rows
+  int16_t* row = coef + (j & 63) * MP3G_LINES;
+#else
   int16_t* row = coef + j * MP3G_LINES;
+#endif
   LineWriter out{row, {}};
   if (J.sf_kind == MP3G_SF_NONE) {  // absent channel of a mono granule
     return 0;

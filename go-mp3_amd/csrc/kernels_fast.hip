@@ -47,24 +47,35 @@ hipError_t fast_kernel_attributes(hipFuncAttributes* a, int* waves_per_block) {
 
 hipError_t launch_fast(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_granule* d_gran,
                        const int16_t* d_coef, const mp3g_state* d_state_in, mp3g_state* d_state_out,
-                       int16_t* d_pcm, unsigned long long* d_stamps, uint32_t* d_hot, hipStream_t stream) {
+                       int16_t* d_pcm, unsigned long long* d_stamps, uint32_t* d_hot, const ZoneScratch* zones,
+                       hipStream_t stream) {
   if (n_chunks == 0) return hipSuccess;
   const dim3 grid((n_chunks + v3::kWaves - 1) / v3::kWaves), block(64 * v3::kWaves);
-  if (d_stamps)
+  ChunkDesc* zl = zones ? zones->list : nullptr;
+  uint32_t* zc = zones ? zones->counts : nullptr;
+  const uint32_t cap = zones ? zones->cap : 0u;
+  if (d_stamps)  // (diagnostic: zones in the wave, no list)
     hipLaunchKernelGGL(v3::granule_fast_kernel<true>, grid, block, 0, stream, d_chunks, n_chunks, d_gran, d_coef,
-                       d_state_in, d_state_out, d_pcm, d_stamps, nullptr);
+                       d_state_in, d_state_out, d_pcm, d_stamps, nullptr, nullptr, nullptr, 0u);
   else if (d_hot)
     hipLaunchKernelGGL((v3::granule_fast_kernel<false, true>), grid, block, 0, stream, d_chunks, n_chunks, d_gran,
-                       d_coef, d_state_in, d_state_out, d_pcm, nullptr, d_hot);
+                       d_coef, d_state_in, d_state_out, d_pcm, nullptr, d_hot, zl, zc, cap);
   else
     hipLaunchKernelGGL(v3::granule_fast_kernel<false>, grid, block, 0, stream, d_chunks, n_chunks, d_gran, d_coef,
-                       d_state_in, d_state_out, d_pcm, nullptr, nullptr);
+                       d_state_in, d_state_out, d_pcm, nullptr, nullptr, zl, zc, cap);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || !zones || d_stamps) return e;
+  // the zone launch: the exact v4 kernel over the list, its waves taking zone
+  // after zone (at most two workgroups per CU; an empty list ends at once)
+  const uint32_t blocks = std::max(1u, std::min<uint32_t>((cap + v4::kXWaves - 1) / v4::kXWaves, 512u));
+  hipLaunchKernelGGL(v4::granule_wexact_kernel<true>, dim3(blocks), dim3(64 * v4::kXWaves), 0, stream, zl, cap, d_gran,
+                     d_coef, d_state_in, d_state_out, d_pcm, zones->counts);
   return hipGetLastError();
 }
 
 hipError_t wexact_kernel_attributes(hipFuncAttributes* a, int* waves_per_block) {
   *waves_per_block = v4::kXWaves;
-  return hipFuncGetAttributes(a, reinterpret_cast<const void*>(&v4::granule_wexact_kernel));
+  return hipFuncGetAttributes(a, reinterpret_cast<const void*>(&v4::granule_wexact_kernel<false>));
 }
 
 hipError_t launch_wexact(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_granule* d_gran,
@@ -72,8 +83,8 @@ hipError_t launch_wexact(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3
                          int16_t* d_pcm, hipStream_t stream) {
   if (n_chunks == 0) return hipSuccess;
   const dim3 grid((n_chunks + v4::kXWaves - 1) / v4::kXWaves), block(64 * v4::kXWaves);
-  hipLaunchKernelGGL(v4::granule_wexact_kernel, grid, block, 0, stream, d_chunks, n_chunks, d_gran, d_coef,
-                     d_state_in, d_state_out, d_pcm);
+  hipLaunchKernelGGL(v4::granule_wexact_kernel<false>, grid, block, 0, stream, d_chunks, n_chunks, d_gran, d_coef,
+                     d_state_in, d_state_out, d_pcm, nullptr);
   return hipGetLastError();
 }
 
@@ -89,7 +100,8 @@ hipError_t launch_synth(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g
 hipError_t launch_fast_stamped(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_granule* d_gran,
                                const int16_t* d_coef, const mp3g_state* d_state_in, mp3g_state* d_state_out,
                                int16_t* d_pcm, unsigned long long* d_stamps, hipStream_t stream) {
-  return launch_fast(d_chunks, n_chunks, d_gran, d_coef, d_state_in, d_state_out, d_pcm, d_stamps, nullptr, stream);
+  return launch_fast(d_chunks, n_chunks, d_gran, d_coef, d_state_in, d_state_out, d_pcm, d_stamps, nullptr, nullptr,
+                     stream);
 }
 
 }  // namespace mp3g

@@ -255,9 +255,9 @@ int mp3g::plan_chunks(int device, const mp3g_stream* streams, uint32_t n_streams
 // hot-granule counters, or null).
 int mp3g::plan_launch(uint32_t mode, const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_granule* d_gran,
                       const int16_t* d_coef, const mp3g_state* d_state_in, mp3g_state* d_state_out, int16_t* d_pcm,
-                      uint32_t* d_hot, hipStream_t stream) {
+                      uint32_t* d_hot, const ZoneScratch* zones, hipStream_t stream) {
   HIP_TRY(launch_granule(plan_variant(mode), d_chunks, n_chunks, d_gran, d_coef, d_state_in, d_state_out, d_pcm,
-                         d_hot, stream));
+                         d_hot, zones, stream));
   return MP3G_OK;
 }
 
@@ -266,8 +266,12 @@ struct mp3g_plan {
   uint32_t mode = 0;
   uint32_t n_streams = 0;
   std::vector<ChunkDesc> chunks;
-  ChunkDesc* d_chunks = nullptr;  // the chunk table, then kHotCounters counters (d_hot)
+  // one device allocation: the chunk table, kHotCounters counters (d_hot),
+  // then (fast mode) the zone scratch of the deferred hot zones
+  ChunkDesc* d_chunks = nullptr;
   uint32_t* d_hot = nullptr;
+  void* d_zones = nullptr;
+  uint32_t zone_cap = 0;
   uint64_t n_granules = 0;
   uint64_t n_halo = 0;
 };
@@ -366,16 +370,22 @@ int mp3g_plan_create(int device, const mp3g_stream* streams, uint32_t n_streams,
   p->mode = mode;
   p->n_streams = n_streams;
   DeviceGuard guard(device);
-  // the chunk table, and the fast kernel's hot-granule counters after it
+  // the chunk table, the fast kernel's hot-granule counters after it, then
+  // the zone scratch (one zone per chunk: more per chunk fall back to the wave)
   const size_t tb = p->chunks.size() * sizeof(ChunkDesc);
-  hipError_t e = hipMalloc(&p->d_chunks, tb + kHotCounters * sizeof(uint32_t));
+  const bool fast = plan_variant(mode) == kVariantFast;
+  p->zone_cap = fast ? (uint32_t)std::max<size_t>(64, p->chunks.size()) : 0u;
+  const size_t zb = fast ? zone_scratch_bytes(p->zone_cap) : 0;
+  const size_t hb = 32;  // kHotCounters, padded
+  hipError_t e = hipMalloc(&p->d_chunks, tb + hb + zb);
   if (e != hipSuccess) {
     delete p;
     return fail(MP3G_ERR_OUT_OF_MEMORY, "hipMalloc(chunks)", e);
   }
   p->d_hot = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(p->d_chunks) + tb);
+  if (fast) p->d_zones = reinterpret_cast<uint8_t*>(p->d_chunks) + tb + hb;
   if (tb) e = hipMemcpy(p->d_chunks, p->chunks.data(), tb, hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemset(p->d_hot, 0, kHotCounters * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMemset(p->d_hot, 0, hb + (zb ? 32 : 0));  // counters, zone counts
   if (e != hipSuccess) {
     (void)hipFree(p->d_chunks);
     delete p;
@@ -414,22 +424,24 @@ int mp3g_plan_execute(mp3g_plan* p, const mp3g_granule* d_gran, const int16_t* d
   for (const ChunkDesc& c : p->chunks) {
     if ((c.flags & kChunkStateOut) && !d_state_out) return fail(MP3G_ERR_INVALID_ARGUMENT, "state_out needed");
   }
-  return plan_launch(p->mode, p->d_chunks, (uint32_t)p->chunks.size(), d_gran, d_coef, d_state_in, d_state_out, d_pcm,
-                     (p->mode & MP3G_FLAG_HOT_STATS) ? p->d_hot : nullptr, static_cast<hipStream_t>(hip_stream));
+  ZoneScratch zs{};
+  if (p->d_zones) zs = zone_scratch_at(p->d_zones, p->zone_cap);
+  return plan_launch(p->mode, p->d_chunks, (uint32_t)p->chunks.size(), d_gran, d_coef, d_state_in, d_state_out,
+                     d_pcm, (p->mode & MP3G_FLAG_HOT_STATS) ? p->d_hot : nullptr, p->d_zones ? &zs : nullptr,
+                     static_cast<hipStream_t>(hip_stream));
 }
 
-// The fast kernel's hot-granule counters of this plan, summed over its
-// launches since creation or the last reset (granule_fast.hip: granules whose
-// PCM the reference-order pass rewrote, granules it ran including the replay
-// of their entry state, and hot granules it met).  Synchronous.
-int mp3g_plan_hot_stats(mp3g_plan* p, uint64_t* out3, int reset) {
-  if (!p || !out3) return fail(MP3G_ERR_INVALID_ARGUMENT, "null argument");
+// The fast kernel's hot-granule counters of this plan (MP3G_FLAG_HOT_STATS),
+// summed over its launches since creation or the last reset (kernels.h
+// kHotCounters).  Synchronous.
+int mp3g_plan_hot_stats(mp3g_plan* p, uint64_t* out4, int reset) {
+  if (!p || !out4) return fail(MP3G_ERR_INVALID_ARGUMENT, "null argument");
   DeviceGuard guard(p->device);
   if (guard.err != hipSuccess) return fail(MP3G_ERR_NO_DEVICE, "hipSetDevice", guard.err);
   uint32_t h[kHotCounters] = {};
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpy(h, p->d_hot, sizeof(h), hipMemcpyDeviceToHost));
-  for (int i = 0; i < 3; i++) out3[i] = h[i];
+  for (int i = 0; i < kHotCounters; i++) out4[i] = h[i];
   if (reset) HIP_TRY(hipMemset(p->d_hot, 0, sizeof(h)));
   return MP3G_OK;
 }

@@ -613,12 +613,12 @@ class Plan:
     def hot_stats(self, reset=False):
         """Fast plans created with FLAG_HOT_STATS: the hot-granule fallback's
         work summed over this plan's launches (mp3g_plan_hot_stats,
-        synchronous): granules whose PCM the
-        reference-order pass rewrote, granules it ran (with the replays of
-        their entry state), hot granules it met."""
-        out = (C.c_uint64 * 3)()
+        synchronous): granules whose PCM the reference-order pass rewrites,
+        hot zones, hot granules the fast pass flagged, granules re-run inside
+        a chunk's own wave (zones beyond the plan's zone list)."""
+        out = (C.c_uint64 * 4)()
         _check(lib().mp3g_plan_hot_stats(self._h, out, 1 if reset else 0))
-        return {"rewritten": out[0], "run": out[1], "hot": out[2]}
+        return {"rewritten": out[0], "zones": out[1], "hot": out[2], "in_wave": out[3]}
 
     PHASES = ("params", "requantize", "stereo+antialias", "imdct", "S rows (transpose)",
               "dct32 (matrixing)", "window+store", "history")

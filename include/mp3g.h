@@ -201,15 +201,19 @@ int mp3g_plan_synth_execute(mp3g_plan* plan, const mp3g_granule* d_granules,
                             mp3g_state* d_state_out, int16_t* d_pcm, void* hip_stream);
 
 /* Fast-mode plans: the work of the hot-granule fallback (granules whose
- * hybrid output exceeds the fast transforms' magnitude bound run again in the
- * reference's operation order), summed over the plan's
- * launches since creation or the last reset, for plans created with
- * MP3G_FLAG_HOT_STATS (others: always 0).  out3[0]: granules whose PCM that
- * pass rewrote; out3[1]: granules it ran, the replays of their entry state
- * included; out3[2]: hot granules it met.  Synchronises the device; reset != 0
- * zeroes the counters after reading.  No reference counterpart: go-mp3 has one
- * arithmetic (frame.go:140-688). */
-int mp3g_plan_hot_stats(mp3g_plan* plan, uint64_t* out3, int reset);
+ * hybrid output exceeds the fast transforms' magnitude bound are decoded
+ * again in the reference's operation order), summed over
+ * the plan's launches since creation or the last reset, for plans created
+ * with MP3G_FLAG_HOT_STATS (others: always 0).  out4[0]: granules whose PCM
+ * that pass rewrites; out4[1]: hot zones (runs of such granules); out4[2]: hot
+ * granules the fast pass flagged; out4[3]: granules re-run inside a chunk's
+ * own wave (zones beyond the plan's zone list, replays included).
+ * Synchronises the device; reset != 0 zeroes the counters after reading.
+ * A fast-mode plan's launches share its zone list (emptied by each launch
+ * itself: graph replays are fine): executions of one plan must be ordered
+ * (one stream, or synchronised between streams).  No reference
+ * counterpart: go-mp3 has one arithmetic (frame.go:140-688). */
+int mp3g_plan_hot_stats(mp3g_plan* plan, uint64_t* out4, int reset);
 
 /* ---- synchronous host-buffer decode (the cgo drop-in entry) --------------
  * Copies the batch to `device`, decodes it and copies PCM (and state_out)
