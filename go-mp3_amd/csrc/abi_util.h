@@ -26,5 +26,5 @@ int plan_chunks(int device, const mp3g_stream* streams, uint32_t n_streams, uint
 struct ZoneScratch;  // kernels.h
 int plan_launch(uint32_t mode, const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_granule* d_gran,
                 const int16_t* d_coef, const mp3g_state* d_state_in, mp3g_state* d_state_out, int16_t* d_pcm,
-                uint32_t* d_hot, const ZoneScratch* zones, hipStream_t stream);
+                const ZoneScratch* zones, hipStream_t stream);
 }  // namespace mp3g

@@ -998,15 +998,19 @@ __device__ __forceinline__ void record_hot(Smem& s, uint32_t& nz, const mp3g_gra
 // to `stamps` (kPhases per workgroup); never used for output.
 constexpr int kPhases = 8;
 // kHotCount: the build of MP3G_FLAG_HOT_STATS plans -- the hot-zone pass adds
-// its work to hot_count (kHotCounters); a separate instantiation because the
-// counting alone cost the production kernel ~1.5 % (register allocation).
+// its work to the counters in aux (kHotCounters); a separate instantiation
+// because the counting alone cost the production kernel ~1.5 % (register
+// allocation).
 template <bool kStamp, bool kHotCount = false>
 __global__ void __launch_bounds__(kLanes * kWaves, MP3G_FAST_WAVES_PER_SIMD)
 granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, const mp3g_granule* __restrict__ gran,
                     const int16_t* __restrict__ coef, const mp3g_state* __restrict__ state_in,
                     mp3g_state* __restrict__ state_out, int16_t* __restrict__ pcm,
-                    unsigned long long* __restrict__ stamps, uint32_t* __restrict__ hot_count,
-                    ChunkDesc* __restrict__ zone_list, uint32_t* __restrict__ zone_count, uint32_t zone_cap) {
+                    void* __restrict__ aux_arg) {
+  // one pointer argument for both: kStamp builds' stamp array, the zone
+  // scratch otherwise (an argument more cost the granule loop SGPRs)
+  unsigned long long* const stamps = kStamp ? static_cast<unsigned long long*>(aux_arg) : nullptr;
+  uint32_t* const aux = kStamp ? nullptr : static_cast<uint32_t*>(aux_arg);
   unsigned long long ph[kPhases] = {}, tprev = 0, rt[4] = {};
   if constexpr (kStamp) rt[0] = __builtin_amdgcn_s_memrealtime();
   auto stamp = [&](int p) {
@@ -1648,7 +1652,15 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
   //      The in-wave pass below is the fallback when the list is full (and
   //      the path of the diagnostic builds, which pass no list). ----
   bool in_wave = nz != 0;
-  if (nz && zone_list) {
+  // aux (kernels.h ZoneScratch): [0] zones listed, [2] the list's capacity,
+  // [4..7] the hot-granule counters (kHotCount builds), the list from byte 32
+  // (one pointer: the three fields as arguments of their own cost the granule
+  // loop SGPRs, 26 spilled instead of 15, +1 % at c3)
+  uint32_t* const hot_count = aux ? aux + 4 : nullptr;
+  if (nz && aux) {
+    uint32_t* const zone_count = aux;
+    ChunkDesc* const zone_list = reinterpret_cast<ChunkDesc*>(aux + 8);
+    const uint32_t zone_cap = __builtin_amdgcn_readfirstlane(aux[2]);
     uint32_t base = 0;
     if (lane_fresh() == 0) base = atomicAdd(zone_count, nz);
     base = __builtin_amdgcn_readfirstlane(base);  // lane 0 is the first active lane
@@ -1720,7 +1732,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     }
     if (done >= end) export_state(zst);
     // (rare: one vector atomic per counter from lane 0 of a chunk with zones)
-    if (kHotCount && lane_fresh() == 0) {
+    if (kHotCount && hot_count && lane_fresh() == 0) {
       atomicAdd(hot_count + 0, n_out);
       atomicAdd(hot_count + 1, nz);
       atomicAdd(hot_count + 2, n_flagged);

@@ -224,9 +224,10 @@ __device__ __forceinline__ void wexact_chunk(const ChunkDesc& cd, const mp3g_gra
 // kZones: the zone launch of a fast-mode plan (kernels_fast.hip launch_fast):
 // `chunks` is the zone list the fast kernel filled -- hot zones as chunks of
 // their own, to be decoded in the reference's order -- with its length in
-// zone_counts[0] (n_chunks = the list's capacity).  The waves take zone after
-// zone; the last workgroup to finish (zone_counts[1] counts them) empties the
-// list for the next launch, after every workgroup has read its length.  An
+// zone_counts[0] (n_chunks = the list's capacity; kernels.h ZoneScratch).
+// The waves take zone after zone; the last workgroup to finish
+// (zone_counts[1] counts them) empties the list for the next launch, after
+// every workgroup has read its length.  An
 // empty list ends every workgroup at once and leaves the counters alone, so
 // the launch pair needs no host-side state (graph replays included).
 template <bool kZones = false>

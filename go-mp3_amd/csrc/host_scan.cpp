@@ -216,6 +216,7 @@ struct PipeBufs {
   // the fast kernel's deferred hot zones (kernels.h ZoneScratch), used by the
   // launches on `comp` in order
   DevMem d_zones;
+  uint32_t zone_cap = 0;
   // the pipeline's streams and per-slot events (created once per device)
   hipStream_t up = nullptr, comp = nullptr, down = nullptr;
   hipEvent_t h2d[2] = {}, kern[2] = {}, d2h[2] = {};
@@ -526,9 +527,11 @@ int mp3g_decode_streams_into(int device, uint32_t n_streams, const uint8_t* cons
   // transfers are the pipeline's fill, the PCM copy-out its steady state)
   uint32_t G = n_groups ? n_groups : (uint32_t)std::min<uint64_t>(32, std::max<uint64_t>(1, total / 131072));
   G = std::max(1u, std::min(G, n_streams));
+  // (the first group half the size of the others: it is the pipeline's fill,
+  // scanned and uploaded before any PCM can leave)
   std::vector<uint32_t> cut{0};
   for (uint32_t k = 0; k < n_streams && cut.size() < G; k++)
-    if (g_at[k + 1] * G >= total * cut.size() && k + 1 < n_streams) cut.push_back(k + 1);
+    if (g_at[k + 1] * (2 * (uint64_t)G - 1) >= total * (2 * cut.size() - 1) && k + 1 < n_streams) cut.push_back(k + 1);
   cut.push_back(n_streams);
   const size_t ng_groups = cut.size() - 1;
   uint64_t max_ng = 0, max_md = 0;
@@ -592,13 +595,15 @@ int mp3g_decode_streams_into(int device, uint32_t n_streams, const uint8_t* cons
     }
     if (rc == MP3G_OK && !B->d_coef.reserve(max_ng * MP3G_COEF_PER_GRANULE * sizeof(int16_t)))
       rc = abi_fail(MP3G_ERR_DEVICE, "decode_streams_into: buffers");
-    const uint32_t zone_cap = (uint32_t)std::max<uint64_t>(64, max_ng);
-    if (rc == MP3G_OK && B->d_zones.bytes < zone_scratch_bytes(zone_cap)) {
-      // a fresh list: both counts zero
-      if (!B->d_zones.reserve(zone_scratch_bytes(zone_cap)) || hipMemset(B->d_zones.p, 0, 32) != hipSuccess)
+    // (a group's plan has at most one chunk per granule: max_ng chunks)
+    const uint32_t zone_cap = (uint32_t)std::min<uint64_t>(kZoneListPerChunk * std::max<uint64_t>(8, max_ng),
+                                                           0xffffffffu);
+    if (rc == MP3G_OK && B->zone_cap < zone_cap) {
+      if (!B->d_zones.reserve(zone_scratch_bytes(zone_cap)) || zone_scratch_init(B->d_zones.p, zone_cap) != hipSuccess)
         rc = abi_fail(MP3G_ERR_DEVICE, "decode_streams_into: buffers");
+      else
+        B->zone_cap = zone_cap;
     }
-    const uint32_t zone_cap_all = (uint32_t)std::min<size_t>((B->d_zones.bytes - 32) / sizeof(ChunkDesc), 0xffffffffu);
     trace.mark("buffers");
     hipStream_t up = B->up, comp = B->comp, down = B->down;
     std::vector<ChunkDesc> chunks;
@@ -682,11 +687,11 @@ int mp3g_decode_streams_into(int device, uint32_t n_streams, const uint8_t* cons
                                    static_cast<mp3g_granule*>(B->d_gran[slot].p), static_cast<int16_t*>(B->d_coef.p),
                                    (mode_reads_to_count1(mode) ? MP3G_HUFF_ROWS_COUNT1 : 0u) | stage, comp);
       if (rc == MP3G_OK && !chunks.empty()) {
-        const ZoneScratch zs = zone_scratch_at(B->d_zones.p, zone_cap_all);
-        rc = plan_launch(mode, static_cast<const ChunkDesc*>(B->d_chunks[slot].p), (uint32_t)chunks.size(),
-                         static_cast<const mp3g_granule*>(B->d_gran[slot].p),
+        const ZoneScratch zs{static_cast<uint32_t*>(B->d_zones.p), B->zone_cap};
+        rc = plan_launch(mode & ~(uint32_t)MP3G_FLAG_HOT_STATS, static_cast<const ChunkDesc*>(B->d_chunks[slot].p),
+                         (uint32_t)chunks.size(), static_cast<const mp3g_granule*>(B->d_gran[slot].p),
                          static_cast<const int16_t*>(B->d_coef.p), nullptr, nullptr,
-                         static_cast<int16_t*>(B->d_pcm[slot].p), nullptr, &zs, comp);
+                         static_cast<int16_t*>(B->d_pcm[slot].p), &zs, comp);
       }
       if (rc) break;
       e = hipEventRecord(B->kern[slot], comp);

@@ -37,30 +37,32 @@ constexpr int kVariantFast = 3;
 constexpr int kVariantExact4 = 4;
 // The hot zones of a fast-mode launch (granule_fast.hip): the fast kernel
 // appends each chunk's zones -- granules whose PCM depends on a hot granule's
-// hybrid output -- to `list` as chunks of their own, counting them in
-// counts[0]; a second launch (the exact v4 kernel over the list) decodes them
-// in the reference's order and, when its last workgroup is done
-// (counts[1]), empties the list for the next launch.  A chunk whose zones do
-// not fit the list's `cap` decodes them in its own wave.  Device memory of
-// the plan (or pipeline) that owns it, zero when allocated; launches that
-// share it must be stream-ordered.
+// hybrid output -- to the list as chunks of their own, counting them; a
+// second launch (the exact v4 kernel over the list) decodes them in the
+// reference's order and, when its last workgroup is done, empties the list
+// for the next launch.  kZoneListPerChunk zones per chunk (the fast kernel's
+// own limit) never overflow it; a chunk whose zones do not fit a smaller list
+// decodes them in its own wave.  Device memory of the plan (or pipeline) that
+// owns it, laid out as
+//   uint32 [0] zones listed, [1] zone-launch workgroups done, [2] capacity,
+//   [3] unused, [4..7] hot-granule counters (kHotCounters), then the list
+// (zone_scratch_init writes a fresh one); launches that share it must be
+// stream-ordered.
+constexpr uint32_t kZoneListPerChunk = 8;
 struct ZoneScratch {
-  uint32_t* counts;  // [2]: zones listed, zone-launch workgroups done
-  ChunkDesc* list;   // [cap]
+  uint32_t* aux;  // the header above; the list at aux + 8
   uint32_t cap;
 };
-// Bytes of zone scratch for `cap` zones (counts padded to 32 B, then the list).
 inline size_t zone_scratch_bytes(uint32_t cap) { return 32 + (size_t)cap * sizeof(ChunkDesc); }
-inline ZoneScratch zone_scratch_at(void* p, uint32_t cap) {
-  return {static_cast<uint32_t*>(p), reinterpret_cast<ChunkDesc*>(static_cast<uint8_t*>(p) + 32), cap};
-}
-// d_hot: kHotCounters counters the fast kernel adds its hot-granule work to
-// (or null; the other kernels ignore it); zones: the fast kernel's deferred
-// hot zones (or null: every chunk redoes its zones in its own wave)
+// Zero header + capacity (synchronous; once per allocation).
+hipError_t zone_scratch_init(void* p, uint32_t cap);
+// zones: the fast kernel's deferred hot zones (or null: every chunk redoes
+// its zones in its own wave); hot_stats: run the counting build, which adds
+// its hot-granule work to the scratch's counters (the other kernels ignore both)
 hipError_t launch_granule(int variant, const ChunkDesc* d_chunks, uint32_t n_chunks,
                           const mp3g_granule* d_gran, const int16_t* d_coef,
                           const mp3g_state* d_state_in, mp3g_state* d_state_out, int16_t* d_pcm,
-                          uint32_t* d_hot, const ZoneScratch* zones, hipStream_t stream);
+                          const ZoneScratch* zones, bool hot_stats, hipStream_t stream);
 // The fast kernel's hot-granule counters (granule_fast.hip, MP3G_FLAG_HOT_STATS):
 // [0] granules whose PCM the reference-order pass rewrites, [1] hot zones,
 // [2] hot granules the fast pass flagged, [3] granules re-run inside a wave
@@ -101,7 +103,7 @@ hipError_t upload_fast_tables(const FastTables& fast, const float* req);
 hipError_t fast_kernel_attributes(hipFuncAttributes* a, int* waves_per_block);
 hipError_t launch_fast(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_granule* d_gran,
                        const int16_t* d_coef, const mp3g_state* d_state_in, mp3g_state* d_state_out,
-                       int16_t* d_pcm, unsigned long long* d_stamps, uint32_t* d_hot, const ZoneScratch* zones,
+                       int16_t* d_pcm, unsigned long long* d_stamps, const ZoneScratch* zones, bool hot_stats,
                        hipStream_t stream);
 
 // Exact mode v4 (granule_wexact.hip, same TU as the fast kernel).

@@ -73,10 +73,10 @@ int chunks_per_cu(int variant) {
 hipError_t launch_granule(int variant, const ChunkDesc* d_chunks, uint32_t n_chunks,
                           const mp3g_granule* d_gran, const int16_t* d_coef,
                           const mp3g_state* d_state_in, mp3g_state* d_state_out, int16_t* d_pcm,
-                          uint32_t* d_hot, const ZoneScratch* zones, hipStream_t stream) {
+                          const ZoneScratch* zones, bool hot_stats, hipStream_t stream) {
   if (n_chunks == 0) return hipSuccess;
   if (variant == kVariantFast)
-    return launch_fast(d_chunks, n_chunks, d_gran, d_coef, d_state_in, d_state_out, d_pcm, nullptr, d_hot, zones,
+    return launch_fast(d_chunks, n_chunks, d_gran, d_coef, d_state_in, d_state_out, d_pcm, nullptr, zones, hot_stats,
                        stream);
   if (variant == kVariantExact4)
     return launch_wexact(d_chunks, n_chunks, d_gran, d_coef, d_state_in, d_state_out, d_pcm, stream);

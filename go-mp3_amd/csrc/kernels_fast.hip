@@ -45,31 +45,37 @@ hipError_t fast_kernel_attributes(hipFuncAttributes* a, int* waves_per_block) {
   return hipFuncGetAttributes(a, reinterpret_cast<const void*>(&v3::granule_fast_kernel<false>));
 }
 
+hipError_t zone_scratch_init(void* p, uint32_t cap) {
+  uint32_t h[8] = {0, 0, cap, 0, 0, 0, 0, 0};
+  return hipMemcpy(p, h, sizeof(h), hipMemcpyHostToDevice);
+}
+
 hipError_t launch_fast(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_granule* d_gran,
                        const int16_t* d_coef, const mp3g_state* d_state_in, mp3g_state* d_state_out,
-                       int16_t* d_pcm, unsigned long long* d_stamps, uint32_t* d_hot, const ZoneScratch* zones,
+                       int16_t* d_pcm, unsigned long long* d_stamps, const ZoneScratch* zones, bool hot_stats,
                        hipStream_t stream) {
   if (n_chunks == 0) return hipSuccess;
   const dim3 grid((n_chunks + v3::kWaves - 1) / v3::kWaves), block(64 * v3::kWaves);
-  ChunkDesc* zl = zones ? zones->list : nullptr;
-  uint32_t* zc = zones ? zones->counts : nullptr;
-  const uint32_t cap = zones ? zones->cap : 0u;
+  uint32_t* aux = zones ? zones->aux : nullptr;
   if (d_stamps)  // (diagnostic: zones in the wave, no list)
     hipLaunchKernelGGL(v3::granule_fast_kernel<true>, grid, block, 0, stream, d_chunks, n_chunks, d_gran, d_coef,
-                       d_state_in, d_state_out, d_pcm, d_stamps, nullptr, nullptr, nullptr, 0u);
-  else if (d_hot)
+                       d_state_in, d_state_out, d_pcm, static_cast<void*>(d_stamps));
+  else if (hot_stats && aux)
     hipLaunchKernelGGL((v3::granule_fast_kernel<false, true>), grid, block, 0, stream, d_chunks, n_chunks, d_gran,
-                       d_coef, d_state_in, d_state_out, d_pcm, nullptr, d_hot, zl, zc, cap);
+                       d_coef, d_state_in, d_state_out, d_pcm, static_cast<void*>(aux));
   else
     hipLaunchKernelGGL(v3::granule_fast_kernel<false>, grid, block, 0, stream, d_chunks, n_chunks, d_gran, d_coef,
-                       d_state_in, d_state_out, d_pcm, nullptr, nullptr, zl, zc, cap);
+                       d_state_in, d_state_out, d_pcm, static_cast<void*>(aux));
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !zones || d_stamps) return e;
   // the zone launch: the exact v4 kernel over the list, its waves taking zone
-  // after zone (at most two workgroups per CU; an empty list ends at once)
-  const uint32_t blocks = std::max(1u, std::min<uint32_t>((cap + v4::kXWaves - 1) / v4::kXWaves, 512u));
-  hipLaunchKernelGGL(v4::granule_wexact_kernel<true>, dim3(blocks), dim3(64 * v4::kXWaves), 0, stream, zl, cap, d_gran,
-                     d_coef, d_state_in, d_state_out, d_pcm, zones->counts);
+  // after zone; one workgroup of 8 waves per 64 chunks of the launch, at most
+  // two per CU (an empty list ends every workgroup at once: the fewer, the
+  // cheaper -- c2's 4,096 chunks get 64)
+  const uint32_t blocks = std::max(16u, std::min<uint32_t>(n_chunks / 64, 512u));
+  hipLaunchKernelGGL(v4::granule_wexact_kernel<true>, dim3(blocks), dim3(64 * v4::kXWaves), 0, stream,
+                     reinterpret_cast<const ChunkDesc*>(aux + 8), zones->cap, d_gran, d_coef, d_state_in,
+                     d_state_out, d_pcm, aux);
   return hipGetLastError();
 }
 
@@ -100,7 +106,7 @@ hipError_t launch_synth(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g
 hipError_t launch_fast_stamped(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_granule* d_gran,
                                const int16_t* d_coef, const mp3g_state* d_state_in, mp3g_state* d_state_out,
                                int16_t* d_pcm, unsigned long long* d_stamps, hipStream_t stream) {
-  return launch_fast(d_chunks, n_chunks, d_gran, d_coef, d_state_in, d_state_out, d_pcm, d_stamps, nullptr, nullptr,
+  return launch_fast(d_chunks, n_chunks, d_gran, d_coef, d_state_in, d_state_out, d_pcm, d_stamps, nullptr, false,
                      stream);
 }
 

@@ -255,9 +255,9 @@ int mp3g::plan_chunks(int device, const mp3g_stream* streams, uint32_t n_streams
 // hot-granule counters, or null).
 int mp3g::plan_launch(uint32_t mode, const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_granule* d_gran,
                       const int16_t* d_coef, const mp3g_state* d_state_in, mp3g_state* d_state_out, int16_t* d_pcm,
-                      uint32_t* d_hot, const ZoneScratch* zones, hipStream_t stream) {
+                      const ZoneScratch* zones, hipStream_t stream) {
   HIP_TRY(launch_granule(plan_variant(mode), d_chunks, n_chunks, d_gran, d_coef, d_state_in, d_state_out, d_pcm,
-                         d_hot, zones, stream));
+                         zones, (mode & MP3G_FLAG_HOT_STATS) != 0, stream));
   return MP3G_OK;
 }
 
@@ -266,10 +266,9 @@ struct mp3g_plan {
   uint32_t mode = 0;
   uint32_t n_streams = 0;
   std::vector<ChunkDesc> chunks;
-  // one device allocation: the chunk table, kHotCounters counters (d_hot),
-  // then (fast mode) the zone scratch of the deferred hot zones
+  // one device allocation: the chunk table, then (fast mode) the zone scratch
+  // of the deferred hot zones with the hot-granule counters in its header
   ChunkDesc* d_chunks = nullptr;
-  uint32_t* d_hot = nullptr;
   void* d_zones = nullptr;
   uint32_t zone_cap = 0;
   uint64_t n_granules = 0;
@@ -370,22 +369,23 @@ int mp3g_plan_create(int device, const mp3g_stream* streams, uint32_t n_streams,
   p->mode = mode;
   p->n_streams = n_streams;
   DeviceGuard guard(device);
-  // the chunk table, the fast kernel's hot-granule counters after it, then
-  // the zone scratch (one zone per chunk: more per chunk fall back to the wave)
-  const size_t tb = p->chunks.size() * sizeof(ChunkDesc);
+  // the chunk table, then the zone scratch (as many zones as the fast kernel
+  // can record per chunk: the list never overflows)
+  const size_t tb = (p->chunks.size() * sizeof(ChunkDesc) + 255) & ~(size_t)255;
   const bool fast = plan_variant(mode) == kVariantFast;
-  p->zone_cap = fast ? (uint32_t)std::max<size_t>(64, p->chunks.size()) : 0u;
+  p->zone_cap = fast ? (uint32_t)std::min<size_t>(kZoneListPerChunk * std::max<size_t>(8, p->chunks.size()),
+                                                  0xffffffffu)
+                     : 0u;
   const size_t zb = fast ? zone_scratch_bytes(p->zone_cap) : 0;
-  const size_t hb = 32;  // kHotCounters, padded
-  hipError_t e = hipMalloc(&p->d_chunks, tb + hb + zb);
+  hipError_t e = hipMalloc(&p->d_chunks, std::max<size_t>(tb + zb, 256));
   if (e != hipSuccess) {
     delete p;
     return fail(MP3G_ERR_OUT_OF_MEMORY, "hipMalloc(chunks)", e);
   }
-  p->d_hot = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(p->d_chunks) + tb);
-  if (fast) p->d_zones = reinterpret_cast<uint8_t*>(p->d_chunks) + tb + hb;
-  if (tb) e = hipMemcpy(p->d_chunks, p->chunks.data(), tb, hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemset(p->d_hot, 0, hb + (zb ? 32 : 0));  // counters, zone counts
+  if (fast) p->d_zones = reinterpret_cast<uint8_t*>(p->d_chunks) + tb;
+  if (!p->chunks.empty()) e = hipMemcpy(p->d_chunks, p->chunks.data(), p->chunks.size() * sizeof(ChunkDesc),
+                                        hipMemcpyHostToDevice);
+  if (e == hipSuccess && fast) e = zone_scratch_init(p->d_zones, p->zone_cap);
   if (e != hipSuccess) {
     (void)hipFree(p->d_chunks);
     delete p;
@@ -424,11 +424,9 @@ int mp3g_plan_execute(mp3g_plan* p, const mp3g_granule* d_gran, const int16_t* d
   for (const ChunkDesc& c : p->chunks) {
     if ((c.flags & kChunkStateOut) && !d_state_out) return fail(MP3G_ERR_INVALID_ARGUMENT, "state_out needed");
   }
-  ZoneScratch zs{};
-  if (p->d_zones) zs = zone_scratch_at(p->d_zones, p->zone_cap);
+  const ZoneScratch zs{static_cast<uint32_t*>(p->d_zones), p->zone_cap};
   return plan_launch(p->mode, p->d_chunks, (uint32_t)p->chunks.size(), d_gran, d_coef, d_state_in, d_state_out,
-                     d_pcm, (p->mode & MP3G_FLAG_HOT_STATS) ? p->d_hot : nullptr, p->d_zones ? &zs : nullptr,
-                     static_cast<hipStream_t>(hip_stream));
+                     d_pcm, p->d_zones ? &zs : nullptr, static_cast<hipStream_t>(hip_stream));
 }
 
 // The fast kernel's hot-granule counters of this plan (MP3G_FLAG_HOT_STATS),
@@ -439,10 +437,13 @@ int mp3g_plan_hot_stats(mp3g_plan* p, uint64_t* out4, int reset) {
   DeviceGuard guard(p->device);
   if (guard.err != hipSuccess) return fail(MP3G_ERR_NO_DEVICE, "hipSetDevice", guard.err);
   uint32_t h[kHotCounters] = {};
+  for (int i = 0; i < kHotCounters; i++) out4[i] = 0;
+  if (!p->d_zones) return MP3G_OK;  // an exact-mode plan: no fallback to count
+  uint32_t* hot = static_cast<uint32_t*>(p->d_zones) + 4;  // kernels.h ZoneScratch header
   HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpy(h, p->d_hot, sizeof(h), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(h, hot, sizeof(h), hipMemcpyDeviceToHost));
   for (int i = 0; i < kHotCounters; i++) out4[i] = h[i];
-  if (reset) HIP_TRY(hipMemset(p->d_hot, 0, sizeof(h)));
+  if (reset) HIP_TRY(hipMemset(hot, 0, sizeof(h)));
   return MP3G_OK;
 }
 

@@ -156,6 +156,40 @@ def test_decode_streams_into_pipelined(gpu, sample_files, n_groups):
     assert st[8] == 8 and 0 < s[8]["n_granules"] < s[9]["n_granules"]
 
 
+def test_decode_streams_into_fast_concurrent(gpu, sample_files):
+    """The three-stream pipeline in fast mode (the main-data kernel, the fast
+    kernel and its zone launch per group) from two host threads at once --
+    one call takes the device's cached buffer set, the other a private one
+    with its own streams and events -- and again on the cached set: the PCM
+    of every call equals the whole-batch mp3g_decode_streams (fast mode is
+    chunking-invariant), at 1, 5 and the automatic number of groups."""
+    import threading
+    import torch
+    from mp3g import synth
+    datas = [synth.encode_stream(71 + k, 40 + 17 * k, p_mixed=0.2, p_is=0.3) for k in range(9)]
+    datas += [sample_files["classic_lame.mp3"], sample_files["mpeg2.mp3"]]
+    want, ws, wst = gpu.decode_streams(datas, mode=gpu.MODE_FAST)
+    n_all = int(sum(int(x["n_granules"]) for x in ws))
+    results = {}
+
+    def run(key, n_groups):
+        out = torch.zeros(n_all * 1152, dtype=torch.int16).pin_memory()
+        n, s, st = gpu.decode_streams_into(datas, out, mode=gpu.MODE_FAST, n_groups=n_groups)
+        results[key] = (n, out.numpy().reshape(-1, 576, 2).copy(), list(st))
+
+    ts = [threading.Thread(target=run, args=(k, g)) for k, g in (("a", 5), ("b", 1))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    run("c", 0)
+    gpu.lib().mp3g_release_cached_buffers()
+    for key in "abc":
+        n, pcm, st = results[key]
+        assert n == n_all and st == list(wst), key
+        assert np.array_equal(pcm, want), key
+
+
 def test_rows_to_count1(gpu, sample_files):
     """MP3G_HUFF_ROWS_COUNT1 (mp3g_huffman_execute_ex): over a poisoned buffer
     each row equals the full-row decode up to its count1 + 5 lines (the

@@ -9,7 +9,7 @@ timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 tail -2 gpurun_out/${T}_pytest.log
 for rep in 1 2; do
   for lib in libmp3g.so libmp3g_r04.so; do
-    MP3G_LIB=$PWD/go-mp3_amd/mp3g/$lib timeout -k 10 300 python bench.py --config c3 --steps 10 --warmup 5 --single-mode --no-cpu-baseline --no-bitstream --no-polyphase > gpurun_out/${T}_ab_${lib}_$rep.json 2> gpurun_out/${T}_ab_${lib}_$rep.err || { tail -5 gpurun_out/${T}_ab_${lib}_$rep.err; exit 1; }
+    MP3G_LIB=$PWD/go-mp3_amd/mp3g/$lib timeout -k 10 300 python bench.py --config c3 --steps 10 --warmup 5 --single-mode --no-cpu-baseline --no-bitstream --no-polyphase --hot-fracs 0.0006,0.006,0.06 > gpurun_out/${T}_ab_${lib}_$rep.json 2> gpurun_out/${T}_ab_${lib}_$rep.err || { tail -5 gpurun_out/${T}_ab_${lib}_$rep.err; exit 1; }
     python - gpurun_out/${T}_ab_${lib}_$rep.json $lib <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
