@@ -441,23 +441,34 @@ def polyphase_leg(args, rank, dev, stream, d_g, streams, n_gran, local):
     return out
 
 
-PROFILE_TAG = "r04"  # profiles/<tag>_<cfg>_<kernel>.json of the current kernels
+PROFILE_TAG = "r05"  # profiles/<tag>_<cfg>_<kernel>.json of the current kernels
 
 
 def profiled_issue(cfg, kernel):
-    """VALU issue utilisation and LDS conflict cycles per LDS instruction of the
-    kernel in the newest profile of the current set (tools/summarize_profile.py),
-    or None."""
+    """What binds the kernel instead of HBM, from the kept
+    profiles of the current set: VALU issue utilisation and LDS conflict
+    cycles per LDS instruction (tools/summarize_profile.py), and the SQ stall
+    split of the headline launches (tools/summarize_stall.py: issuing / ready
+    but not issued / parked on s_waitcnt, shares of the wave cycles), or None."""
     import glob
+    out = None
     for f in sorted(glob.glob(os.path.join(REPO, "profiles", f"{PROFILE_TAG}_{cfg}_*.json"))):
+        if f.endswith("_stall.json"):
+            continue
         d = json.load(open(f))
         if kernel.split("::")[-1] in d.get("kernel", "") and d.get("valu_issue_util") is not None:
             sq = d.get("sq", {})
-            return {"valu_issue_util": round(d["valu_issue_util"], 3),
-                    "lds_conflict_cycles_per_op": round(sq.get("SQ_LDS_BANK_CONFLICT", 0.0) /
-                                                        max(sq.get("SQ_INSTS_LDS", 1.0), 1.0), 3),
-                    "source": os.path.relpath(f, REPO)}
-    return None
+            out = {"valu_issue_util": round(d["valu_issue_util"], 3),
+                   "lds_conflict_cycles_per_op": round(sq.get("SQ_LDS_BANK_CONFLICT", 0.0) /
+                                                       max(sq.get("SQ_INSTS_LDS", 1.0), 1.0), 3),
+                   "source": os.path.relpath(f, REPO)}
+            break
+    st = os.path.join(REPO, "profiles", f"{PROFILE_TAG}_{cfg}_{kernel.split('::')[-1]}_stall.json")
+    if os.path.exists(st):
+        d = json.load(open(st))
+        out = dict(out or {}, stall_split=d["split"], stall_source=os.path.relpath(st, REPO),
+                   instructions_per_wave=d.get("instructions_per_wave"))
+    return out
 
 
 def profiled_traffic(cfg, kernel):

@@ -32,6 +32,13 @@ __device__ float g_req[4][8207];
 #include "granule_synth.hip"
 #include "granule_wexact.hip"
 
+#ifndef MP3G_ZONE_LAUNCH
+#define MP3G_ZONE_LAUNCH 1  // 0: timing experiments only (hot zones in the chunk's own wave)
+#endif
+#ifndef MP3G_ZONE_CHUNKS_PER_WG
+#define MP3G_ZONE_CHUNKS_PER_WG 64  // zone-launch workgroups: one per this many chunks (16 .. 512)
+#endif
+
 namespace mp3g {
 
 hipError_t upload_fast_tables(const FastTables& fast, const float* req) {
@@ -56,6 +63,7 @@ hipError_t launch_fast(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_
                        hipStream_t stream) {
   if (n_chunks == 0) return hipSuccess;
   const dim3 grid((n_chunks + v3::kWaves - 1) / v3::kWaves), block(64 * v3::kWaves);
+  if (!MP3G_ZONE_LAUNCH) zones = nullptr;  // (A/B builds: round 4's in-wave zones)
   uint32_t* aux = zones ? zones->aux : nullptr;
   if (d_stamps)  // (diagnostic: zones in the wave, no list)
     hipLaunchKernelGGL(v3::granule_fast_kernel<true>, grid, block, 0, stream, d_chunks, n_chunks, d_gran, d_coef,
@@ -72,7 +80,7 @@ hipError_t launch_fast(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_
   // after zone; one workgroup of 8 waves per 64 chunks of the launch, at most
   // two per CU (an empty list ends every workgroup at once: the fewer, the
   // cheaper -- c2's 4,096 chunks get 64)
-  const uint32_t blocks = std::max(16u, std::min<uint32_t>(n_chunks / 64, 512u));
+  const uint32_t blocks = std::max(16u, std::min<uint32_t>(n_chunks / MP3G_ZONE_CHUNKS_PER_WG, 512u));
   hipLaunchKernelGGL(v4::granule_wexact_kernel<true>, dim3(blocks), dim3(64 * v4::kXWaves), 0, stream,
                      reinterpret_cast<const ChunkDesc*>(aux + 8), zones->cap, d_gran, d_coef, d_state_in,
                      d_state_out, d_pcm, aux);

@@ -218,3 +218,41 @@ def test_kernel_variants_agree(gpu, captured, variant):
     want, _ = oracle.dsp_streams(g, c, s)
     pcm, _ = run_plan(gpu, g, c, s, chunk=3, mode=mode)
     assert_pcm_equal(pcm, want, variant + " synth")
+
+
+def test_c3_full_size_properties(gpu):
+    """BASELINE config c3 at FULL size (1,024 seeded streams x 1,024 frames,
+    2,097,152 granules, the bench's workload) through size-independent
+    properties: the exact kernel equals the oracle on a sample of streams
+    spread over the batch; the fast kernel is within 1 LSB of the exact one on
+    every sample of the batch (differing in < 1 % of them); fast mode is
+    chunking-invariant (the automatic plan and 256-granule chunks give the
+    same bytes); and the hot-granule fallback finds nothing to redo."""
+    import torch
+    _, g, c, s = synth.encode_batch(range(1, 1025), 1024, n_threads=16)
+    n = len(g)
+    assert n == 2097152
+    dev = torch.device("cuda:0")
+    d_g = torch.from_numpy(g.view(np.uint8).copy()).to(dev)
+    d_c = torch.from_numpy(c.view(np.uint8).reshape(-1).copy()).to(dev)
+    h = torch.cuda.current_stream(dev).cuda_stream
+    outs = {}
+    for key, mode, chunk in (("exact", gpu.MODE_EXACT, 0), ("fast", gpu.MODE_FAST | gpu.FLAG_HOT_STATS, 0),
+                             ("fast256", gpu.MODE_FAST, 256)):
+        d_p = torch.empty(n * 1152, dtype=torch.int16, device=dev)
+        plan = gpu.Plan(s, granules_per_chunk=chunk, mode=mode)
+        plan.execute(d_g, d_c, d_p, stream=h)
+        torch.cuda.synchronize(dev)
+        if key == "fast":
+            assert plan.hot_stats() == {"rewritten": 0, "zones": 0, "hot": 0, "in_wave": 0}
+        plan.close()
+        outs[key] = d_p
+    assert torch.equal(outs["fast"], outs["fast256"]), "fast mode depends on the chunking"
+    d = (outs["fast"].to(torch.int32) - outs["exact"].to(torch.int32)).abs()
+    assert int(d.max()) <= 1 and float((d > 0).float().mean()) < 0.01
+    per = 2048
+    for k in (0, 341, 682, 1023):  # streams across the batch against the oracle
+        lo = k * per
+        want, _ = oracle.dsp_streams(g[lo:lo + per], c[lo:lo + per], gpu.streams_for([per]))
+        got = outs["exact"][lo * 1152:(lo + per) * 1152].cpu().numpy().reshape(per, 576, 2)
+        assert_pcm_equal(got, want, f"c3 stream {k}")
