@@ -221,12 +221,34 @@ struct PipeBufs {
   hipStream_t up = nullptr, comp = nullptr, down = nullptr;
   hipEvent_t h2d[2] = {}, kern[2] = {}, d2h[2] = {};
   bool ensure_sync() {
-    for (hipStream_t* q : {&up, &comp, &down})
+    if (!down && !create_down()) return false;
+    for (hipStream_t* q : {&up, &comp})
       if (!*q && hipStreamCreateWithFlags(q, hipStreamNonBlocking) != hipSuccess) return false;
     for (int i = 0; i < 2; i++)
       for (hipEvent_t* ev : {&h2d[i], &kern[i], &d2h[i]})
         if (!*ev && hipEventCreateWithFlags(ev, hipEventDisableTiming) != hipSuccess) return false;
     return true;
+  }
+  // The PCM copy-out's stream.  HIP runs these device -> pinned-host copies
+  // as blit kernels (__amd_rocclr_copyBuffer) while the upload is on the DMA
+  // engine, and unrestricted the blit's waves took the CUs the next group's
+  // main-data kernel needed (0.14 -> 5.9 ms per group, r05i timeline): the
+  // copy-out stream is limited to a share of the CUs, spread over the XCDs
+  // (MP3G_PIPE_DOWN_CUS: that many CUs, 0 = unrestricted).
+  bool create_down() {
+    int dev = 0, ncu = 0;
+    const char* env = std::getenv("MP3G_PIPE_DOWN_CUS");
+    int want = env ? std::atoi(env) : 32;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      ncu = 0;
+    if (want <= 0 || ncu <= 0 || want >= ncu) return hipStreamCreateWithFlags(&down, hipStreamNonBlocking) == hipSuccess;
+    std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
+    for (int i = 0; i < want; i++) {
+      const int cu = (int)((int64_t)i * ncu / want);
+      mask[(size_t)cu / 32] |= 1u << (cu % 32);
+    }
+    return hipExtStreamCreateWithCUMask(&down, (uint32_t)mask.size(), mask.data()) == hipSuccess;
   }
   ~PipeBufs() {
     for (hipStream_t q : {up, comp, down})
