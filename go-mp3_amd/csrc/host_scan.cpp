@@ -229,19 +229,22 @@ struct PipeBufs {
         if (!*ev && hipEventCreateWithFlags(ev, hipEventDisableTiming) != hipSuccess) return false;
     return true;
   }
-  // The PCM copy-out's stream.  HIP runs these device -> pinned-host copies
-  // as blit kernels (__amd_rocclr_copyBuffer) while the upload is on the DMA
-  // engine, and unrestricted the blit's waves took the CUs the next group's
-  // main-data kernel needed (0.14 -> 5.9 ms per group, r05i timeline): the
-  // copy-out stream is limited to a share of the CUs, spread over the XCDs
-  // (MP3G_PIPE_DOWN_CUS: that many CUs, 0 = unrestricted).
+  // The PCM copy-out's stream, limited to a few CUs spread over the XCDs
+  // (MP3G_PIPE_DOWN_CUS: that many, 0 = unrestricted).  Into pinned memory the
+  // copy-out is a kernel of ours (launch_copy_out: 54-55 GB/s from 16 CUs,
+  // where hipMemcpyAsync's DMA engine moved 30 GB/s without a profiler and a
+  // blit kernel under one: tools/copy_exp.hip); restricted, it leaves the
+  // decode kernels the other CUs (an unrestricted blit had stretched the
+  // main-data kernel 0.14 -> 5.9 ms per group, the r05i timeline).
+  int down_cus = 0;
   bool create_down() {
     int dev = 0, ncu = 0;
     const char* env = std::getenv("MP3G_PIPE_DOWN_CUS");
-    int want = env ? std::atoi(env) : 32;
+    int want = env ? std::atoi(env) : 16;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       ncu = 0;
+    down_cus = want > 0 && want < ncu ? want : ncu > 0 ? ncu : 256;
     if (want <= 0 || ncu <= 0 || want >= ncu) return hipStreamCreateWithFlags(&down, hipStreamNonBlocking) == hipSuccess;
     std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0u);
     for (int i = 0; i < want; i++) {
@@ -628,6 +631,16 @@ int mp3g_decode_streams_into(int device, uint32_t n_streams, const uint8_t* cons
     }
     trace.mark("buffers");
     hipStream_t up = B->up, comp = B->comp, down = B->down;
+    // the caller's PCM buffer: pinned and 16-B aligned -> our copy kernel
+    // writes it through its device address; anything else -> hipMemcpyAsync
+    int16_t* pcm_dev = nullptr;
+    {
+      hipPointerAttribute_t pa;
+      if ((reinterpret_cast<uintptr_t>(pcm) & 15u) == 0 && hipPointerGetAttributes(&pa, pcm) == hipSuccess &&
+          pa.type == hipMemoryTypeHost && pa.devicePointer)
+        pcm_dev = static_cast<int16_t*>(pa.devicePointer);
+      (void)hipGetLastError();  // (pageable memory: an "invalid value" to clear)
+    }
     std::vector<ChunkDesc> chunks;
     for (size_t gi = 0; gi < ng_groups && rc == MP3G_OK; gi++) {
       const int slot = (int)(gi & 1);
@@ -719,7 +732,10 @@ int mp3g_decode_streams_into(int device, uint32_t n_streams, const uint8_t* cons
       e = hipEventRecord(B->kern[slot], comp);
       // down
       if (e == hipSuccess) e = hipStreamWaitEvent(down, B->kern[slot], 0);
-      if (e == hipSuccess)
+      if (e == hipSuccess && pcm_dev)
+        e = launch_copy_out(B->d_pcm[slot].p, pcm_dev + G0 * (MP3G_PCM_BYTES_PER_GRANULE / sizeof(int16_t)),
+                            ng * MP3G_PCM_BYTES_PER_GRANULE, 8 * B->down_cus, down);
+      else if (e == hipSuccess)
         e = hipMemcpyAsync(pcm + G0 * (MP3G_PCM_BYTES_PER_GRANULE / sizeof(int16_t)), B->d_pcm[slot].p,
                            ng * MP3G_PCM_BYTES_PER_GRANULE, hipMemcpyDeviceToHost, down);
       if (e == hipSuccess) e = hipEventRecord(B->d2h[slot], down);

@@ -69,6 +69,11 @@ hipError_t launch_granule(int variant, const ChunkDesc* d_chunks, uint32_t n_chu
 // (zones that did not fit the zone list, with their replays).
 constexpr int kHotCounters = 4;
 
+// Copy of `bytes` (a multiple of 16; both pointers 16-B aligned) from device
+// memory to device-accessible pinned host memory (`dst`: its device address)
+// by a kernel of `blocks` 256-thread workgroups (kernels.hip).
+hipError_t launch_copy_out(const void* d_src, void* dst, size_t bytes, int blocks, hipStream_t stream);
+
 // Chunks of `variant` resident per CU (one per wave for the fast kernel, one
 // per workgroup for the exact kernels), from the kernel's VGPR / LDS usage.
 int chunks_per_cu(int variant);

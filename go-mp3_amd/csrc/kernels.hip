@@ -46,6 +46,25 @@ hipError_t upload_tables(const DspTables& tables) {
   return e;
 }
 
+// PCM copy-out into device-accessible pinned host memory: 16 B per lane,
+// non-temporal.  HIP's own device -> host hipMemcpyAsync runs on a DMA engine
+// at ~30 GB/s on MI355X; this kernel writes the same pinned buffer at
+// 54-55 GB/s from as few as 16 CUs (tools/copy_exp.hip), so the pipelined
+// drop-in runs it on a stream limited to a few CUs beside the decode kernels.
+typedef unsigned int copy_u4 __attribute__((ext_vector_type(4)));
+__global__ void __launch_bounds__(256) pcm_copy_out_kernel(const copy_u4* __restrict__ src, copy_u4* __restrict__ dst,
+                                                           size_t n16) {
+  for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256)
+    __builtin_nontemporal_store(src[i], &dst[i]);
+}
+
+hipError_t launch_copy_out(const void* d_src, void* dst, size_t bytes, int blocks, hipStream_t stream) {
+  if (!bytes) return hipSuccess;
+  hipLaunchKernelGGL(pcm_copy_out_kernel, dim3(std::max(1, blocks)), dim3(256), 0, stream,
+                     static_cast<const copy_u4*>(d_src), static_cast<copy_u4*>(dst), bytes / 16);
+  return hipGetLastError();
+}
+
 int chunks_per_cu(int variant) {
   hipFuncAttributes a;
   hipError_t e;
