@@ -143,6 +143,9 @@ struct __align__(16) WaveSmem {
   uint32_t zone[8][2];
 };
 constexpr uint32_t kZones = 8;
+// the plan's zone list holds kZoneListPerChunk zones per chunk (kernels.h): a
+// wave records at most kZones, so the list cannot overflow
+static_assert(kZones <= kZoneListPerChunk, "zone list smaller than a chunk's zones");
 
 // Raw coefficients of lane (ch, sb) of granule g: its 18 lines, 36 B at
 // coef[g][ch][18 sb], as 9 dwords (two int16 each) by three 12-B buffer loads
@@ -1649,15 +1652,16 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
   // ---- hot zones (rare), deferred: appended to the launch's zone list as
   //      chunks of their own, which the exact v4 kernel then decodes in the
   //      reference's order over many waves (launch_fast: the zone launch).
-  //      The in-wave pass below is the fallback when the list is full (and
-  //      the path of the diagnostic builds, which pass no list). ----
-  bool in_wave = nz != 0;
+  //      The list has room for every zone of every chunk (kZoneListPerChunk),
+  //      so the production builds carry no in-wave pass (and no scratch: its
+  //      registers spilled 1.9 KB per lane); the in-wave pass below runs in
+  //      the diagnostic (kStamp) builds only, which pass no list. ----
   // aux (kernels.h ZoneScratch): [0] zones listed, [2] the list's capacity,
   // [4..7] the hot-granule counters (kHotCount builds), the list from byte 32
   // (one pointer: the three fields as arguments of their own cost the granule
   // loop SGPRs, 26 spilled instead of 15, +1 % at c3)
   uint32_t* const hot_count = aux ? aux + 4 : nullptr;
-  if (nz && aux) {
+  if (!kStamp && nz) {
     uint32_t* const zone_count = aux;
     ChunkDesc* const zone_list = reinterpret_cast<ChunkDesc*>(aux + 8);
     const uint32_t zone_cap = __builtin_amdgcn_readfirstlane(aux[2]);
@@ -1665,40 +1669,31 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     if (lane_fresh() == 0) base = atomicAdd(zone_count, nz);
     base = __builtin_amdgcn_readfirstlane(base);  // lane 0 is the first active lane
     const int zl = lane_fresh();
-    if (base + nz <= zone_cap) {
-      in_wave = false;
-      if ((uint32_t)zl < nz) {
-        const uint32_t zs = s.zone[zl][0], ze = s.zone[zl][1];
-        ChunkDesc z;
-        z.out_first = zs;
-        z.stream_first = cd.stream_first;
-        z.n_out = ze - zs;
-        z.stream = cd.stream;
-        // entry state as the chunk's; the exported state when the zone ends
-        // the chunk (it then overwrites this pass's export)
-        z.flags = (cd.flags & kChunkStateIn) | (ze == end ? (cd.flags & kChunkStateOut) : 0u);
-        z.reserved = 0;
-        zone_list[base + zl] = z;
-      }
-      if constexpr (kHotCount) {
-        uint32_t n_out = 0;
-        for (uint32_t i = 0; i < nz; i++)
-          n_out += __builtin_amdgcn_readfirstlane(s.zone[i][1]) - __builtin_amdgcn_readfirstlane(s.zone[i][0]);
-        if (lane_fresh() == 0) {
-          atomicAdd(hot_count + 0, n_out);
-          atomicAdd(hot_count + 1, nz);
-          atomicAdd(hot_count + 2, n_flagged);
-        }
-      }
-    } else if (base + (uint32_t)zl < zone_cap && (uint32_t)zl < nz) {
-      // the slots this wave took below the capacity hold no zone
-      ChunkDesc z = {};
-      z.out_first = cd.out_first;
+    if ((uint32_t)zl < nz && base + (uint32_t)zl < zone_cap) {  // (always below the capacity: see kZones)
+      const uint32_t zs = s.zone[zl][0], ze = s.zone[zl][1];
+      ChunkDesc z;
+      z.out_first = zs;
       z.stream_first = cd.stream_first;
+      z.n_out = ze - zs;
+      z.stream = cd.stream;
+      // entry state as the chunk's; the exported state when the zone ends
+      // the chunk (it then overwrites this pass's export)
+      z.flags = (cd.flags & kChunkStateIn) | (ze == end ? (cd.flags & kChunkStateOut) : 0u);
+      z.reserved = 0;
       zone_list[base + zl] = z;
     }
+    if constexpr (kHotCount) {
+      uint32_t n_out = 0;
+      for (uint32_t i = 0; i < nz; i++)
+        n_out += __builtin_amdgcn_readfirstlane(s.zone[i][1]) - __builtin_amdgcn_readfirstlane(s.zone[i][0]);
+      if (lane_fresh() == 0) {
+        atomicAdd(hot_count + 0, n_out);
+        atomicAdd(hot_count + 1, nz);
+        atomicAdd(hot_count + 2, n_flagged);
+      }
+    }
   }
-  if (in_wave) {
+  if (kStamp && nz) {
     f2 zst[9];  // the zones' own overlap state (nothing flows in from the fast pass)
     uint32_t done = 0;  // the exact state in zst / the ring is valid for granules < done
     bool have = false;

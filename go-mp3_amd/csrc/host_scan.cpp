@@ -621,13 +621,14 @@ int mp3g_decode_streams_into(int device, uint32_t n_streams, const uint8_t* cons
     if (rc == MP3G_OK && !B->d_coef.reserve(max_ng * MP3G_COEF_PER_GRANULE * sizeof(int16_t)))
       rc = abi_fail(MP3G_ERR_DEVICE, "decode_streams_into: buffers");
     // (a group's plan has at most one chunk per granule: max_ng chunks)
-    const uint32_t zone_cap = (uint32_t)std::min<uint64_t>(kZoneListPerChunk * std::max<uint64_t>(8, max_ng),
-                                                           0xffffffffu);
+    const uint64_t zone_cap = (uint64_t)kZoneListPerChunk * std::max<uint64_t>(8, max_ng);
+    if (rc == MP3G_OK && zone_cap > 0xffffffffu) rc = abi_fail(MP3G_ERR_UNSUPPORTED, "decode_streams_into: group too large");
     if (rc == MP3G_OK && B->zone_cap < zone_cap) {
-      if (!B->d_zones.reserve(zone_scratch_bytes(zone_cap)) || zone_scratch_init(B->d_zones.p, zone_cap) != hipSuccess)
+      if (!B->d_zones.reserve(zone_scratch_bytes((uint32_t)zone_cap)) ||
+          zone_scratch_init(B->d_zones.p, (uint32_t)zone_cap) != hipSuccess)
         rc = abi_fail(MP3G_ERR_DEVICE, "decode_streams_into: buffers");
       else
-        B->zone_cap = zone_cap;
+        B->zone_cap = (uint32_t)zone_cap;
     }
     trace.mark("buffers");
     hipStream_t up = B->up, comp = B->comp, down = B->down;

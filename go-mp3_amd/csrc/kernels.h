@@ -41,8 +41,8 @@ constexpr int kVariantExact4 = 4;
 // second launch (the exact v4 kernel over the list) decodes them in the
 // reference's order and, when its last workgroup is done, empties the list
 // for the next launch.  kZoneListPerChunk zones per chunk (the fast kernel's
-// own limit) never overflow it; a chunk whose zones do not fit a smaller list
-// decodes them in its own wave.  Device memory of the plan (or pipeline) that
+// own limit) never overflow it, and launch_fast refuses a smaller list (the
+// production kernel has no in-wave fallback).  Device memory of the plan (or pipeline) that
 // owns it, laid out as
 //   uint32 [0] zones listed, [1] zone-launch workgroups done, [2] capacity,
 //   [3] unused, [4..7] hot-granule counters (kHotCounters), then the list
@@ -56,8 +56,8 @@ struct ZoneScratch {
 inline size_t zone_scratch_bytes(uint32_t cap) { return 32 + (size_t)cap * sizeof(ChunkDesc); }
 // Zero header + capacity (synchronous; once per allocation).
 hipError_t zone_scratch_init(void* p, uint32_t cap);
-// zones: the fast kernel's deferred hot zones (or null: every chunk redoes
-// its zones in its own wave); hot_stats: run the counting build, which adds
+// zones: the fast kernel's deferred hot zones (required in fast mode, with
+// room for kZoneListPerChunk per chunk: hipErrorInvalidValue otherwise); hot_stats: run the counting build, which adds
 // its hot-granule work to the scratch's counters (the other kernels ignore both)
 hipError_t launch_granule(int variant, const ChunkDesc* d_chunks, uint32_t n_chunks,
                           const mp3g_granule* d_gran, const int16_t* d_coef,

@@ -32,9 +32,6 @@ __device__ float g_req[4][8207];
 #include "granule_synth.hip"
 #include "granule_wexact.hip"
 
-#ifndef MP3G_ZONE_LAUNCH
-#define MP3G_ZONE_LAUNCH 1  // 0: timing experiments only (hot zones in the chunk's own wave)
-#endif
 #ifndef MP3G_ZONE_CHUNKS_PER_WG
 #define MP3G_ZONE_CHUNKS_PER_WG 64  // zone-launch workgroups: one per this many chunks (16 .. 512)
 #endif
@@ -63,7 +60,9 @@ hipError_t launch_fast(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_
                        hipStream_t stream) {
   if (n_chunks == 0) return hipSuccess;
   const dim3 grid((n_chunks + v3::kWaves - 1) / v3::kWaves), block(64 * v3::kWaves);
-  if (!MP3G_ZONE_LAUNCH) zones = nullptr;  // (A/B builds: round 4's in-wave zones)
+  // the production builds defer every hot zone to the plan's zone list: a
+  // fast launch without one is the diagnostic (stamped) build only
+  if (!d_stamps && (!zones || !zones->aux || zones->cap < (uint64_t)kZoneListPerChunk * n_chunks)) return hipErrorInvalidValue;
   uint32_t* aux = zones ? zones->aux : nullptr;
   if (d_stamps)  // (diagnostic: zones in the wave, no list)
     hipLaunchKernelGGL(v3::granule_fast_kernel<true>, grid, block, 0, stream, d_chunks, n_chunks, d_gran, d_coef,

@@ -373,9 +373,12 @@ int mp3g_plan_create(int device, const mp3g_stream* streams, uint32_t n_streams,
   // can record per chunk: the list never overflows)
   const size_t tb = (p->chunks.size() * sizeof(ChunkDesc) + 255) & ~(size_t)255;
   const bool fast = plan_variant(mode) == kVariantFast;
-  p->zone_cap = fast ? (uint32_t)std::min<size_t>(kZoneListPerChunk * std::max<size_t>(8, p->chunks.size()),
-                                                  0xffffffffu)
-                     : 0u;
+  const uint64_t zone_cap = fast ? (uint64_t)kZoneListPerChunk * std::max<size_t>(8, p->chunks.size()) : 0u;
+  if (zone_cap > 0xffffffffu) {
+    delete p;
+    return fail(MP3G_ERR_UNSUPPORTED, "fast-mode plan of more than 2^29 chunks");
+  }
+  p->zone_cap = (uint32_t)zone_cap;
   const size_t zb = fast ? zone_scratch_bytes(p->zone_cap) : 0;
   hipError_t e = hipMalloc(&p->d_chunks, std::max<size_t>(tb + zb, 256));
   if (e != hipSuccess) {

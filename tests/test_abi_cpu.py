@@ -141,6 +141,26 @@ def test_exact_kernel_has_no_fma():
         assert not bad, (name, sorted(set(bad)))
 
 
+def test_production_plan_kernels_use_no_scratch():
+    """The kernels a plan launches in production -- fast v3 (and its counting
+    build), the zone launch / exact v4, the polyphase kernel -- keep every
+    value in registers and LDS: no private segment (a scratch reload's
+    s_waitcnt vmcnt would also wait for the in-flight PCM stores and
+    prefetches).  The stamped diagnostic build may spill."""
+    csrc = os.path.join(REPO, "go-mp3_amd", "csrc")
+    subprocess.check_call(["make", "-s", "-C", csrc, "build/kernels_fast.s"], stderr=subprocess.DEVNULL)
+    meta = open(os.path.join(csrc, "build", "kernels_fast.s")).read().split("amdhsa.kernels:")[-1]
+    rows = re.findall(r"\.name:\s+(\S+)\n(?:.*\n)*?\s+\.private_segment_fixed_size:\s+(\d+)", meta)
+    seen = {n: int(p) for n, p in rows}
+    prod = {n: p for n, p in seen.items()
+            if "granule_fast_kernelILb1E" not in n}  # (kStamp = true: the diagnostic build)
+    assert any("granule_fast_kernelILb0ELb0E" in n for n in prod), sorted(seen)
+    assert any("granule_wexact_kernelILb1E" in n for n in prod), sorted(seen)
+    # the counting build (MP3G_FLAG_HOT_STATS) may hold a dword or two
+    for n, p in prod.items():
+        assert p <= (16 if "ILb0ELb1E" in n else 0), (n, p)
+
+
 def test_decode_streams_into_capacity_check_needs_no_device(sample_files):
     """mp3g_decode_streams_into sizes the output with its header pre-pass
     before it touches a device: too small an output fails with the blocks

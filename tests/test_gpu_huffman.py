@@ -190,6 +190,31 @@ def test_decode_streams_into_fast_concurrent(gpu, sample_files):
         assert np.array_equal(pcm, want), key
 
 
+def test_decode_streams_into_buffer_kinds(gpu):
+    """The PCM copy-out of mp3g_decode_streams_into takes the library's copy
+    kernel into a pinned, 16-B aligned buffer (through its device address,
+    also at an offset inside a pinned allocation) and hipMemcpyAsync
+    otherwise (pinned but 2-B aligned, pageable numpy): the same PCM every
+    time, nothing written outside the buffer's range."""
+    import torch
+    from mp3g import synth
+    datas = [synth.encode_stream(91 + k, 30 + 11 * k) for k in range(5)]
+    want, ws, wst = gpu.decode_streams(datas, mode=gpu.MODE_FAST)
+    n_all = int(sum(int(x["n_granules"]) for x in ws))
+    size = n_all * 1152
+    big = torch.full((size + 64,), 0x5A5A, dtype=torch.int16).pin_memory()
+    for off in (0, 8, 1):  # 16-B aligned (kernel), aligned interior (kernel), 2-B (memcpy)
+        big.fill_(0x5A5A)
+        n, s, st = gpu.decode_streams_into(datas, big[off:off + size], mode=gpu.MODE_FAST, n_groups=2)
+        got = big.numpy()
+        assert n == n_all and list(st) == list(wst), off
+        assert np.array_equal(got[off:off + size].reshape(-1, 576, 2), want), off
+        assert (got[:off] == 0x5A5A).all() and (got[off + size:] == 0x5A5A).all(), off
+    page = np.full(size, 0x5A5A, np.int16)
+    n, s, st = gpu.decode_streams_into(datas, page, mode=gpu.MODE_FAST, n_groups=2)
+    assert n == n_all and np.array_equal(page.reshape(-1, 576, 2), want)
+
+
 def test_rows_to_count1(gpu, sample_files):
     """MP3G_HUFF_ROWS_COUNT1 (mp3g_huffman_execute_ex): over a poisoned buffer
     each row equals the full-row decode up to its count1 + 5 lines (the
