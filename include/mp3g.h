@@ -207,7 +207,8 @@ int mp3g_plan_synth_execute(mp3g_plan* plan, const mp3g_granule* d_granules,
  * with MP3G_FLAG_HOT_STATS (others: always 0).  out4[0]: granules whose PCM
  * that pass rewrites; out4[1]: hot zones (runs of such granules); out4[2]: hot
  * granules the fast pass flagged; out4[3]: granules re-run inside a chunk's
- * own wave (zones beyond the plan's zone list, replays included).
+ * own wave -- always 0 since the zone list holds every chunk's zones (kept
+ * for ABI 5 layout).
  * Synchronises the device; reset != 0 zeroes the counters after reading.
  * A fast-mode plan's launches share its zone list (emptied by each launch
  * itself: graph replays are fine): executions of one plan must be ordered
