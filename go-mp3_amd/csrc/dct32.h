@@ -33,9 +33,10 @@ using pk::bhi;
 using pk::f2;
 using pk::fma2;
 using pk::mk;
-using pk::mulmi;
+using pk::add_mi;
 using pk::post_tw;
-using pk::pre_tw;
+using pk::pre_tw2;
+using pk::sub_mi;
 using pk::swp;
 
 #define MP3G_D32 __host__ __device__ __forceinline__
@@ -79,27 +80,28 @@ constexpr float kC3 = 3.826834324e-01f;   // cos(3 pi/8)
 
 // in-place 4-point complex FFT (forward) of z0..z3
 MP3G_D32 void fft4(f2& z0, f2& z1, f2& z2, f2& z3) {
-  const f2 e0 = z0 + z2, e1 = z0 - z2, o0 = z1 + z3, o1 = mulmi(z1 - z3);
+  const f2 e0 = z0 + z2, e1 = z0 - z2, o0 = z1 + z3, d = z1 - z3;
   z0 = e0 + o0;
   z2 = e0 - o0;
-  z1 = e1 + o1;
-  z3 = e1 - o1;
+  z1 = add_mi(e1, d);  // e1 + (-i) d
+  z3 = sub_mi(e1, d);
 }
 
 // DCT4_16 of d (pairs dp[j] = (d[2j], d[2j+1])) -> 8 output pairs
 MP3G_D32 void dct4_16(const f2 dp[8], f2 out[8]) {
   f2 v[8];
 #pragma unroll
-  for (int n = 0; n < 8; n++) v[n] = pre_tw(dp[n].x, dp[7 - n].y, kPre16[n][0], kPre16[n][1]);
+  for (int n = 0; n < 8; n++) v[n] = pre_tw2<0, 1>(dp[n], dp[7 - n], kPre16[n][0], kPre16[n][1]);
   // 8-point FFT, decimation in time: E = FFT4(v even), O = FFT4(v odd)
   fft4(v[0], v[2], v[4], v[6]);
   fft4(v[1], v[3], v[5], v[7]);
   // V[k] = E[k] + W8^k O[k], V[k+4] = E[k] - W8^k O[k]; W8 = (1 - i)/sqrt2
+  // (o2 = (-i) v5 and o3 = (-i) w7 ride on the adds: add_mi / sub_mi)
   const f2 o0 = v[1];
-  const f2 o1 = (v[3] + mulmi(v[3])) * mk(kR2, kR2);
-  const f2 o2 = mulmi(v[5]);
-  const f2 o3 = mulmi((v[7] + mulmi(v[7])) * mk(kR2, kR2));
-  const f2 V[8] = {v[0] + o0, v[2] + o1, v[4] + o2, v[6] + o3, v[0] - o0, v[2] - o1, v[4] - o2, v[6] - o3};
+  const f2 o1 = add_mi(v[3], v[3]) * mk(kR2, kR2);
+  const f2 w7 = add_mi(v[7], v[7]) * mk(kR2, kR2);
+  const f2 V[8] = {v[0] + o0,          v[2] + o1, add_mi(v[4], v[5]), add_mi(v[6], w7),
+                   v[0] - o0,          v[2] - o1, sub_mi(v[4], v[5]), sub_mi(v[6], w7)};
 #pragma unroll
   for (int k = 0; k < 8; k++) out[k] = post_tw(V[k], kPost16[k][0], kPost16[k][1]);
 }
@@ -108,7 +110,7 @@ MP3G_D32 void dct4_16(const f2 dp[8], f2 out[8]) {
 MP3G_D32 void dct4_8(const f2 bp[4], f2 out[4]) {
   f2 v[4];
 #pragma unroll
-  for (int n = 0; n < 4; n++) v[n] = pre_tw(bp[n].x, bp[3 - n].y, kPre8[n][0], kPre8[n][1]);
+  for (int n = 0; n < 4; n++) v[n] = pre_tw2<0, 1>(bp[n], bp[3 - n], kPre8[n][0], kPre8[n][1]);
   fft4(v[0], v[1], v[2], v[3]);
 #pragma unroll
   for (int k = 0; k < 4; k++) out[k] = post_tw(v[k], kPost8[k][0], kPost8[k][1]);

@@ -87,16 +87,19 @@ __host__ __device__ __forceinline__ void dct4_18(const float x[18], float X[18])
 // The same transform on packed float pairs (pk.h; ~80 v_pk_* instead of ~160
 // scalar operations): P[k] = (X[2k], X[17-2k]), k = 0..8.
 __host__ __device__ __forceinline__ void dft3p(pk::f2& a, pk::f2& b, pk::f2& c) {
-  const pk::f2 s = b + c, d = pk::mulmi(b - c);  // (b - c) * (-i)
+  const pk::f2 s = b + c, d = b - c;  // (the (-i) rotation of d rides on the FMAs)
   const pk::f2 t = pk::fma2(pk::mk(-0.5f, -0.5f), s, a);
   a += s;
-  b = pk::fma2(pk::mk(kH, kH), d, t);
-  c = pk::fma2(pk::mk(-kH, -kH), d, t);
+  b = pk::fma_mi<false>(kH, d, t);  // t + kH (-i) d
+  c = pk::fma_mi<true>(kH, d, t);
 }
 __host__ __device__ __forceinline__ void dct4_18_pk(const float x[18], pk::f2 P[9]) {
   pk::f2 z[9];
 #pragma unroll
-  for (int n = 0; n < 9; n++) z[n] = pk::pre_tw(x[2 * n], x[17 - 2 * n], kPre[n][0], kPre[n][1]);
+  for (int n = 0; n < 9; n++) {
+    const pk::f2 ab = pk::mk(x[2 * n], x[17 - 2 * n]);
+    z[n] = pk::pre_tw2<0, 1>(ab, ab, kPre[n][0], kPre[n][1]);
+  }
 #pragma unroll
   for (int n2 = 0; n2 < 3; n2++) dft3p(z[n2], z[3 + n2], z[6 + n2]);
   z[4] = pk::cmul(z[4], kW[0][0], kW[0][1]);
