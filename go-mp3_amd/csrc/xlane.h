@@ -9,13 +9,14 @@ namespace xl {
 
 __device__ __forceinline__ int dpp_ctrl_wave_shr1() { return 0x138; }
 
-// value of lane l-1 (lane 0: 0)
+// value of lane l-1 (lane 0: 0).  bound_ctrl writes the 0 of the lane with
+// no source itself (an "old" operand of 0 instead costs a v_mov per use)
 __device__ __forceinline__ float from_prev(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, false));
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x138, 0xf, 0xf, true));
 }
 // value of lane l+1 (lane 63: 0)
 __device__ __forceinline__ float from_next(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false));
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130, 0xf, 0xf, true));
 }
 // value of lane l^32 (the other half-wave): v_permlane32_swap swaps the upper
 // half of its first operand with the lower half of its second.
