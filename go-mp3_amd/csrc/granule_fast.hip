@@ -117,7 +117,14 @@ struct __align__(16) SharedSmem {
   // FastTables::lband: read per lane every granule, so it lives in LDS -- a
   // vector global load there would wait (vmcnt is in order) for the previous
   // granule's PCM stores
-  uint32_t lband[kCombos][32];
+  // per subband: .x = lband (first band | bit 5 + j: line j = 1..17 starts a
+  // band), .y = the band-start bits of lines 1..16 with every bit doubled: the
+  // popcount of a prefix is then the byte offset of a float16 exponent, so a
+  // line pair's exponent address is one v_and + one v_bcnt (accumulating the
+  // base) instead of a bit-field extract, a popcount and a shift-add; one
+  // ds_read_b64 reads both
+  uint2 lbd[kCombos][32];
+  __device__ uint32_t lband_at(int c, int k) const { return lbd[c][k].x; }
 };
 // per-wave working set 9.1 KB.  The workgroup (8 waves + shared tables) must
 // stay <= 64 x 1280 B (gfx950 LDS allocation granule) for 2 workgroups
@@ -588,7 +595,7 @@ __device__ __forceinline__ void front_long_fast(float x[18], const uint32_t cw[9
   // lines 1..j.  Every long band starts at an even line (consts.go:68-97
   // SfBandIndices; dsp_tables.cpp checks it), so lines 2q and 2q + 1
   // share one band: one exponent read per line pair.
-  const uint32_t lb = sh.lband[P.combo][k];
+  const uint32_t lb = sh.lband_at(P.combo, k);
   _Float16 ex[9];
 #pragma unroll
   for (int q = 0; q < 9; q++)
@@ -702,7 +709,7 @@ __device__ __forceinline__ void stereo_stage(float x[18], const WS& s, const SH&
 #pragma unroll
     for (int b = 0; b < 14; b++) ns_is += 3 * (int)g_fast.sfb_short[P.combo][b] < c1r;
     if (!short0) {
-      const uint32_t lb = sh.lband[P.combo][k0];
+      const uint32_t lb = sh.lband_at(P.combo, k0);
 #pragma unroll
       for (int j = 0; j < 18; j++) {
         const int sfl = (int)(lb & 31u) + __builtin_popcount((lb >> 5) & ((2u << j) - 1u));
@@ -1039,7 +1046,14 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     // is_pos 0..6 -> isRatios (frame.go:304-306); 7 -> (1, 1): no change
     for (int e = t; e < 16; e += kLanes * kWaves) (&sh.isr[0][0])[e] = e < 14 ? (&g_fast.is_ratio[0][0])[e] : 1.0f;
     for (int e = t; e < 32 * 16; e += kLanes * kWaves) sh.dwin[e >> 4][e & 15] = (&g_fast.dwin[0][0])[e] * 32767.0f;
-    for (int e = t; e < kCombos * 32; e += kLanes * kWaves) (&sh.lband[0][0])[e] = (&g_fast.lband[0][0])[e];
+    for (int e = t; e < kCombos * 32; e += kLanes * kWaves) {
+      const uint32_t lb = (&g_fast.lband[0][0])[e];
+      uint32_t d = 0;
+      // (bit 5 + j of lb: line j = 1..17 starts a band; lines 1..16 doubled
+      // into bits 2 (j - 1), 2 (j - 1) + 1 -- line 17 is odd, never a start)
+      for (int j = 1; j <= 16; j++) d |= ((lb >> (5 + j)) & 1u) * (3u << (2 * (j - 1)));
+      (&sh.lbd[0][0])[e] = make_uint2(lb, d);
+    }
   };
   const int lane = threadIdx.x & (kLanes - 1);
   // wave-uniform in an SGPR: the chunk descriptor then comes in by scalar
@@ -1190,13 +1204,16 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
   const uint32_t span = end - w, span2 = 2 * span, span3 = 3 * span;
   uint32_t nz = 0;  // hot zones recorded (s.zone)
   uint32_t n_flagged = 0;  // hot granules the pass flagged (kHotCount builds)
+  // priority = #{L in 1..3 : 4 (end - g) > L span}: 3 from the start, one
+  // less from granule tL = end - floor(L span / 4) on (three compares per
+  // granule instead of recomputing the level)
+  const uint32_t t3 = end - (span3 >> 2), t2 = end - (span2 >> 2), t1 = end - (span >> 2);
+  if (MP3G_FAST_PRIO) __builtin_amdgcn_s_setprio(3);
   for (uint32_t g = w; g < end; g++) {
     if (MP3G_FAST_PRIO) {
-      const uint32_t left4 = 4u * (end - g);  // priority floor(4 * left / span), 3 .. 0
-      if (left4 > span3) __builtin_amdgcn_s_setprio(3);
-      else if (left4 > span2) __builtin_amdgcn_s_setprio(2);
-      else if (left4 > span) __builtin_amdgcn_s_setprio(1);
-      else __builtin_amdgcn_s_setprio(0);
+      if (g == t1) __builtin_amdgcn_s_setprio(0);
+      else if (g == t2) __builtin_amdgcn_s_setprio(1);
+      else if (g == t3) __builtin_amdgcn_s_setprio(2);
     }
     const bool out = g >= out_first;
     // does a replayed granule's V feed anything? (see v2 / DESIGN.md halo)
@@ -1226,14 +1243,14 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     // ---- per-granule front-end parameters: band exponents (long bands only
     //      when no channel has short blocks) ----
     {
-      // long bands: lane = (c, sfb), 44 lanes
+      // long bands: lane = (ch, sfb = k), k < 22 -- the lane's own channel
+      // parameters d0 / d1 (an absent channel's lanes write values nothing reads)
       const int e = lane_fresh();
-      if (e < 44) {
-        const int c = e >= 22, sfb = e - 22 * c;
-        const uint32_t a0 = c ? cp0[1] : cp0[0], a1 = c ? cp1[1] : cp1[0];
-        const int v = (int)((a0 >> 16) & 0xffu) - 210 -
-                      ((a0 >> 24) ? 4 : 2) * ((int)s.desc.ch[c].scalefac_l[sfb] + (int)(a1 & 0xffu) * kPretab(sfb));
-        s.expo[e] = (_Float16)(0.25f * (float)v);
+      if ((e & 31) < 22) {
+        const int sfb = e & 31;
+        const int v = (int)((d0 >> 16) & 0xffu) - 210 -
+                      ((d0 >> 24) ? 4 : 2) * ((int)s.desc.ch[ch].scalefac_l[sfb] + (int)(d1 & 0xffu) * kPretab(sfb));
+        s.expo[22 * ch + sfb] = (_Float16)(0.25f * (float)v);
       }
       if (!all_long) {
         // short bands: (c, sfb, win), 78 entries
@@ -1267,11 +1284,14 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       // lines 1..j.  Every long band starts at an even line (consts.go:68-97
       // SfBandIndices; dsp_tables.cpp checks it), so lines 2q and 2q + 1
       // share one band: one exponent read per line pair.
-      const uint32_t lb = sh.lband[combo][lane_fresh() & 31];  // (lane recomputed: no spilled address)
+      const int kl = lane_fresh() & 31;  // (lane recomputed: no spilled address)
+      const uint2 lbd = sh.lbd[combo][kl];
+      const uint32_t lb = lbd.x, d2 = lbd.y;
+      const char* eb = reinterpret_cast<const char*>(&s.expo[22 * ch + (int)(lb & 31u)]);
       _Float16 ex[9];
 #pragma unroll
-      for (int q = 0; q < 9; q++)
-        ex[q] = s.expo[22 * ch + (int)(lb & 31u) + __builtin_popcount((lb >> 5) & ((2u << (2 * q)) - 1u))];
+      for (int q = 0; q < 9; q++)  // band starts among lines 1..2q (bits 0..4q-1 of d2)
+        ex[q] = *reinterpret_cast<const _Float16*>(eb + __builtin_popcount(d2 & (q == 8 ? ~0u : (1u << (4 * q)) - 1u)));
       // Lines >= count1 hold zeros (the bitstream parse's guarantee,
       // maindata/huffman.go:130-134; mp3g_validate checks it), and requantizing
       // 0 gives 0, so long blocks need no per-line count1 test here.
@@ -1398,7 +1418,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
 #pragma unroll
         for (int b = 0; b < 14; b++) ns_is += 3 * (int)g_fast.sfb_short[combo][b] < c1r;
         if (!short0) {
-          const uint32_t lb = sh.lband[combo][k0];
+          const uint32_t lb = sh.lbd[combo][k0].x;
 #pragma unroll
           for (int j = 0; j < 18; j++) {
             const int sfl = (int)(lb & 31u) + __builtin_popcount((lb >> 5) & ((2u << j) - 1u));

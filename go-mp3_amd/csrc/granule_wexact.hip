@@ -40,6 +40,7 @@ constexpr int kColV16 = 32;
 struct __align__(16) XSharedSmem {
   float isr[8][2];            // as v3's SharedSmem (stereo_stage)
   uint32_t lband[kCombos][32];
+  __device__ uint32_t lband_at(int c, int k) const { return lband[c][k]; }
   float dwin[32][20];         // window taps (below), rows padded to 20 floats
   float win[4][36];           // imdctWinData (imdct.go:21-57)
 };
