@@ -34,8 +34,6 @@ using pk::f2;
 using pk::fma2;
 using pk::mk;
 using pk::add_mi;
-using pk::post_tw;
-using pk::pre_tw2;
 using pk::sub_mi;
 using pk::swp;
 
@@ -91,7 +89,7 @@ MP3G_D32 void fft4(f2& z0, f2& z1, f2& z2, f2& z3) {
 MP3G_D32 void dct4_16(const f2 dp[8], f2 out[8]) {
   f2 v[8];
 #pragma unroll
-  for (int n = 0; n < 8; n++) v[n] = pre_tw2<0, 1>(dp[n], dp[7 - n], kPre16[n][0], kPre16[n][1]);
+  for (int n = 0; n < 8; n++) v[n] = pk::pre_tw2<0, 1>(dp[n], dp[7 - n], kPre16[n][0], kPre16[n][1]);
   // 8-point FFT, decimation in time: E = FFT4(v even), O = FFT4(v odd)
   fft4(v[0], v[2], v[4], v[6]);
   fft4(v[1], v[3], v[5], v[7]);
@@ -103,17 +101,17 @@ MP3G_D32 void dct4_16(const f2 dp[8], f2 out[8]) {
   const f2 V[8] = {v[0] + o0,          v[2] + o1, add_mi(v[4], v[5]), add_mi(v[6], w7),
                    v[0] - o0,          v[2] - o1, sub_mi(v[4], v[5]), sub_mi(v[6], w7)};
 #pragma unroll
-  for (int k = 0; k < 8; k++) out[k] = post_tw(V[k], kPost16[k][0], kPost16[k][1]);
+  for (int k = 0; k < 8; k++) out[k] = pk::post_tw(V[k], kPost16[k][0], kPost16[k][1]);
 }
 
 // DCT4_8 of b (pairs bp[j] = (b[2j], b[2j+1])) -> 4 output pairs (X[2k], X[7-2k])
 MP3G_D32 void dct4_8(const f2 bp[4], f2 out[4]) {
   f2 v[4];
 #pragma unroll
-  for (int n = 0; n < 4; n++) v[n] = pre_tw2<0, 1>(bp[n], bp[3 - n], kPre8[n][0], kPre8[n][1]);
+  for (int n = 0; n < 4; n++) v[n] = pk::pre_tw2<0, 1>(bp[n], bp[3 - n], kPre8[n][0], kPre8[n][1]);
   fft4(v[0], v[1], v[2], v[3]);
 #pragma unroll
-  for (int k = 0; k < 4; k++) out[k] = post_tw(v[k], kPost8[k][0], kPost8[k][1]);
+  for (int k = 0; k < 4; k++) out[k] = pk::post_tw(v[k], kPost8[k][0], kPost8[k][1]);
 }
 
 // X[m] = sum_k S[k] cos(pi m (2k+1) / 64) for one slot.  sp[j] = (S[2j], S[2j+1]);

@@ -82,10 +82,10 @@ MP3G_PK f2 cmul(f2 z, float c, float d) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const uint64_t cd = cpair(c, d);
   f2 t, r;
-  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(z), "s"(cd));  // (r c, r d)
-  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
-      : "=v"(r)
-      : "v"(z), "s"(cd), "v"(t));  // + (-s d, s c)
+  asm("v_pk_mul_f32 %1, %2, %3 op_sel_hi:[0,1]\n\t"  // (r c, r d)
+      "v_pk_fma_f32 %0, %2, %3, %1 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"  // + (-s d, s c)
+      : "=v"(r), "=&v"(t)
+      : "v"(z), "s"(cd));
   return r;
 #else
   return fma2(bhi(z), mk(-d, c), blo(z) * mk(c, d));
@@ -98,18 +98,17 @@ template <int HA, int HB>
 MP3G_PK f2 pre_tw2(f2 A, f2 B, float c, float s) {
   static_assert((HA == 0 || HA == 1) && (HB == 0 || HB == 1), "half");
 #if defined(__HIP_DEVICE_COMPILE__)
+  static_assert(HA == 0 && HB == 1, "the halves the transforms use");
+  // t = (a c, -a s); r = (b s, b c) + t -- one statement: hipcc pads a wait
+  // state after every inline asm whose outputs a VALU reads next, so the
+  // product and the FMA share a block (a VALU result feeding the next VALU
+  // needs no wait state of its own)
   const uint64_t cs = cpair(c, s);
   f2 t, r;
-  // t = (a c, -a s)
-  if constexpr (HA == 0)
-    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1] neg_hi:[0,1]" : "=v"(t) : "v"(A), "s"(cs));
-  else
-    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,0] neg_hi:[0,1]" : "=v"(t) : "v"(A), "s"(cs));
-  // r = (b s, b c) + t
-  if constexpr (HB == 0)
-    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[0,0,1]" : "=v"(r) : "v"(B), "s"(cs), "v"(t));
-  else
-    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1]" : "=v"(r) : "v"(B), "s"(cs), "v"(t));
+  asm("v_pk_mul_f32 %1, %2, %4 op_sel_hi:[0,1] neg_hi:[0,1]\n\t"
+      "v_pk_fma_f32 %0, %3, %4, %1 op_sel:[1,1,0] op_sel_hi:[1,0,1]"
+      : "=v"(r), "=&v"(t)
+      : "v"(A), "v"(B), "s"(cs));
   return r;
 #else
   return pre_tw(HA ? A.y : A.x, HB ? B.y : B.x, c, s);
@@ -120,10 +119,10 @@ MP3G_PK f2 post_tw(f2 v, float c, float s) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const uint64_t cs = cpair(c, s);
   f2 t, r;
-  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(v), "s"(cs));  // (vr c, vr s)
-  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_hi:[0,1,0]"
-      : "=v"(r)
-      : "v"(v), "s"(cs), "v"(t));  // + (vi s, -vi c)
+  asm("v_pk_mul_f32 %1, %2, %3 op_sel_hi:[0,1]\n\t"  // (vr c, vr s)
+      "v_pk_fma_f32 %0, %2, %3, %1 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_hi:[0,1,0]"  // + (vi s, -vi c)
+      : "=v"(r), "=&v"(t)
+      : "v"(v), "s"(cs));
   return r;
 #else
   return fma2(bhi(v), mk(s, -c), blo(v) * mk(c, s));
