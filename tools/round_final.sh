@@ -1,16 +1,34 @@
 #!/bin/bash
 # End-of-round measurement on ONE box (one gpurun call), so that the kept
-# profiles and the bench line come from the same machine:
+# profiles and the bench line come from the same machine and the line reads
+# the profiles of its own build:
 #   tools/round_final.sh <tag>          e.g. r05
-# 1. GPU tests, smoke, the default bench line (tools/gpu_check.sh <tag>m)
+# 1. GPU tests and smoke
 # 2. rocprofv3 passes of c3 (tools/profile.sh <tag> c3: head / trace / fetch /
 #    write / sq / flops) and the stall split (tools/profile_stall.sh)
-# Summaries: tools/summarize_profile.py, tools/summarize_stall.py (run after
-# the call, on the merged gpurun_out/).
+# 3. their summaries into profiles/ on the box (tools/summarize_round.sh)
+# 4. the default bench line, which reads those profiles (traffic, profile_check,
+#    issue: the same build and box)
+# The summaries travel back under gpurun_out/profiles_<tag>/ (copy them to profiles/).
 set -u
 export TMPDIR=/tmp
 T=${1:-r05}
-bash tools/gpu_check.sh ${T}m || exit 1
+mkdir -p gpurun_out
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/${T}m_pytest.log 2>&1 || { tail -30 gpurun_out/${T}m_pytest.log; exit 1; }
+tail -3 gpurun_out/${T}m_pytest.log
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${T}m_smoke.log 2>&1 || { tail -20 gpurun_out/${T}m_smoke.log; exit 1; }
+tail -1 gpurun_out/${T}m_smoke.log
 bash tools/profile.sh $T c3 || exit 1
 bash tools/profile_stall.sh $T c3 || exit 1
+bash tools/summarize_round.sh $T > gpurun_out/summarize_${T}.log 2>&1 || { tail -20 gpurun_out/summarize_${T}.log; exit 1; }
+mkdir -p gpurun_out/profiles_$T
+cp profiles/${T}_c3_*.json profiles/${T}_c3_*.csv profiles/${T}_flop_calib.json gpurun_out/profiles_$T/
+timeout -k 10 400 python bench.py > gpurun_out/${T}m_bench.json 2> gpurun_out/${T}m_bench.err || { tail -20 gpurun_out/${T}m_bench.err; exit 1; }
+python - "$T" <<'PY'
+import json, sys
+d = json.loads(open(f'gpurun_out/{sys.argv[1]}m_bench.json').read().strip().splitlines()[-1])
+r = d['roofline']
+print(d['value'], d['ms_per_step'], r['frac'], d.get('max_dpcm_lsb'), 'same build:', r.get('traffic_same_build'),
+      'profile:', (r.get('profile') or {}).get('kernel_ms'))
+PY
 echo final done
