@@ -14,7 +14,7 @@ CXXFLAGS="-O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectori
 objs=$(ls "$C"/build/*.o)
 vobjs=""
 for TU in $TUS; do
-  EXTRA=""; [ "$TU" = kernels_fast.hip ] && EXTRA="-mllvm -disable-machine-licm"
+  EXTRA=""; [ "$TU" = kernels_fast.hip ] && EXTRA="-mllvm -disable-machine-licm -mllvm -misched-cluster=0"
   $HIPCC $CXXFLAGS $EXTRA $FLAGS -c "$C/$TU" -o "$B/$TU.o"
   objs=$(echo "$objs" | grep -v "/$TU.o")
   vobjs="$vobjs $B/$TU.o"
