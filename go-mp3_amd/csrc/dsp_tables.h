@@ -101,6 +101,9 @@ struct FastTables {
   uint16_t sfb_long[kCombos][23];
   uint16_t sfb_short[kCombos][14];
   int8_t pretab[22];
+  // the fast kernel's long-block requantize: p43[x + 128] = sign(x) |x|^(4/3)
+  // as float32 (= +-req[0][|x|]) for x = -128..127
+  float p43[256];
 };
 void build_fast_tables(const DspTables& t, FastTables* f);
 

@@ -97,6 +97,9 @@ constexpr int kHist = 16;
 #endif
 constexpr int kSlots = kHist + 18;
 static_assert(kSlots == kFastRingSlots, "FastTables::sinfo indexes the staged ring");
+#ifndef MP3G_P43_SCHED
+#define MP3G_P43_SCHED 0
+#endif
 #ifndef MP3G_FAST_DWIN_STRIDE
 #define MP3G_FAST_DWIN_STRIDE 20
 #endif
@@ -118,13 +121,17 @@ struct __align__(16) SharedSmem {
   // vector global load there would wait (vmcnt is in order) for the previous
   // granule's PCM stores
   // per subband: .x = lband (first band | bit 5 + j: line j = 1..17 starts a
-  // band), .y = the band-start bits of lines 1..16 with every bit doubled: the
-  // popcount of a prefix is then the byte offset of a float16 exponent, so a
-  // line pair's exponent address is one v_and + one v_bcnt (accumulating the
+  // band), .y = the band-start bits of the even lines 2i = 2..16 (only even
+  // lines start a band) at bits 4 (i - 1) .. 4 i - 1, four bits each: the
+  // popcount of a prefix is then the byte offset of a float32 band gain, so a
+  // line pair's gain address is one v_and + one v_bcnt (accumulating the
   // base) instead of a bit-field extract, a popcount and a shift-add; one
   // ds_read_b64 reads both
   uint2 lbd[kCombos][32];
   __device__ uint32_t lband_at(int c, int k) const { return lbd[c][k].x; }
+  // FastTables::p43: sign(x) |x|^(4/3) of x = -128..127 at byte offset
+  // 4 x + 512 -- the long-block requantize is a table read and one multiply
+  float p43[256];
 };
 // per-wave working set 9.1 KB.  The workgroup (8 waves + shared tables) must
 // stay <= 64 x 1280 B (gfx950 LDS allocation granule) for 2 workgroups
@@ -143,8 +150,12 @@ struct __align__(16) WaveSmem {
   // c3 -0.4 % against whole rows, tools/gpu_r03z.sh)
   mp3g_granule descn;
   // requantization exponents n4 / 4 (float16, exact) of the long bands
-  // [ch][sfb] and short bands [ch][sfb][win]
+  // [ch][sfb] and short bands [ch][sfb][win]; in the fast loop's all-long
+  // granules the long bands' gains 2^(n4 / 4) as float32 [ch][sfb] instead
+  // (expo_gain(): the first 176 of these 244 bytes)
   _Float16 expo[2 * 22 + 2 * 39];
+  __device__ float* expo_gain() { return reinterpret_cast<float*>(expo); }
+  __device__ const float* expo_gain() const { return reinterpret_cast<const float*>(expo); }
   // hot-granule zones [start, end) of this chunk, recorded by the fast pass
   // and redone in the reference's order after it (kHotS)
   uint32_t zone[8][2];
@@ -287,6 +298,13 @@ __device__ __forceinline__ float requant_fast(int xi, _Float16 e) {
   const float xf = (float)xi;
   const float t = __builtin_fmaf(__builtin_amdgcn_logf(fabsf(xf)), 1.0f / 3.0f, (float)e);
   return xf * __builtin_amdgcn_exp2f(t);
+}
+
+// sign(x) |x|^(4/3) g of the int16 in the low half of xw (the long-block
+// requantize's lanes outside the p43 table)
+__device__ __forceinline__ float requant_gain(uint32_t xw, float g) {
+  const float xf = (float)(int16_t)xw;
+  return xf * __builtin_amdgcn_exp2f(__builtin_amdgcn_logf(fabsf(xf)) * (1.0f / 3.0f)) * g;
 }
 
 // The lane id, recomputed where it is used (asm volatile: not hoisted out of
@@ -1030,8 +1048,15 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       tprev = t;
     }
   };
-  __shared__ SharedSmem sh;
-  __shared__ WaveSmem wsm[kWaves];
+  // one block, the shared tables first: the p43 table then sits below 64 KiB
+  // (its address is a ds_read's immediate offset) and every offset its
+  // discarded reads can form stays inside the workgroup's LDS
+  __shared__ struct {
+    SharedSmem sh;
+    WaveSmem w[kWaves];
+  } lds;
+  SharedSmem& sh = lds.sh;
+  WaveSmem* const wsm = lds.w;
   // the workgroup's tables, filled after each wave has issued its first
   // loads: their latencies overlap
   auto shared_init = [&]() {
@@ -1049,11 +1074,12 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     for (int e = t; e < kCombos * 32; e += kLanes * kWaves) {
       const uint32_t lb = (&g_fast.lband[0][0])[e];
       uint32_t d = 0;
-      // (bit 5 + j of lb: line j = 1..17 starts a band; lines 1..16 doubled
-      // into bits 2 (j - 1), 2 (j - 1) + 1 -- line 17 is odd, never a start)
-      for (int j = 1; j <= 16; j++) d |= ((lb >> (5 + j)) & 1u) * (3u << (2 * (j - 1)));
+      // (bit 5 + j of lb: line j = 1..17 starts a band; line 2i = 2..16 into
+      // bits 4 (i - 1) .. 4 i - 1 -- odd lines never start one)
+      for (int i = 1; i <= 8; i++) d |= ((lb >> (5 + 2 * i)) & 1u) * (15u << (4 * (i - 1)));
       (&sh.lbd[0][0])[e] = make_uint2(lb, d);
     }
+    for (int e = t; e < 256; e += kLanes * kWaves) sh.p43[e] = g_fast.p43[e];
   };
   const int lane = threadIdx.x & (kLanes - 1);
   // wave-uniform in an SGPR: the chunk descriptor then comes in by scalar
@@ -1250,7 +1276,8 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
         const int sfb = e & 31;
         const int v = (int)((d0 >> 16) & 0xffu) - 210 -
                       ((d0 >> 24) ? 4 : 2) * ((int)s.desc.ch[ch].scalefac_l[sfb] + (int)(d1 & 0xffu) * kPretab(sfb));
-        s.expo[22 * ch + sfb] = (_Float16)(0.25f * (float)v);
+        if (all_long) s.expo_gain()[22 * ch + sfb] = __builtin_amdgcn_exp2f(0.25f * (float)v);
+        else s.expo[22 * ch + sfb] = (_Float16)(0.25f * (float)v);
       }
       if (!all_long) {
         // short bands: (c, sfb, win), 78 entries
@@ -1274,30 +1301,53 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     // the lane's 18 line-info words and raw integers are loaded in bulk first
     float x[18];
     if (all_long) {
-      int xi[18];
-#pragma unroll
-      for (int q = 0; q < 9; q++) {
-        xi[2 * q] = (int)(int16_t)(cw[q] & 0xffffu);
-        xi[2 * q + 1] = (int)(int16_t)(cw[q] >> 16);
-      }
       // long band of line j: first band of the subband + band starts among
       // lines 1..j.  Every long band starts at an even line (consts.go:68-97
       // SfBandIndices; dsp_tables.cpp checks it), so lines 2q and 2q + 1
-      // share one band: one exponent read per line pair.
+      // share one band: one gain read per line pair.
       const int kl = lane_fresh() & 31;  // (lane recomputed: no spilled address)
       const uint2 lbd = sh.lbd[combo][kl];
-      const uint32_t lb = lbd.x, d2 = lbd.y;
-      const char* eb = reinterpret_cast<const char*>(&s.expo[22 * ch + (int)(lb & 31u)]);
-      _Float16 ex[9];
+      const uint32_t lb = lbd.x, d4 = lbd.y;
+      const char* eb = reinterpret_cast<const char*>(&s.expo_gain()[22 * ch + (int)(lb & 31u)]);
+      float gq[9];
 #pragma unroll
-      for (int q = 0; q < 9; q++)  // band starts among lines 1..2q (bits 0..4q-1 of d2)
-        ex[q] = *reinterpret_cast<const _Float16*>(eb + __builtin_popcount(d2 & (q == 8 ? ~0u : (1u << (4 * q)) - 1u)));
+      for (int q = 0; q < 9; q++)  // band starts among lines 2..2q (bits 0..4q-1 of d4)
+        gq[q] = *reinterpret_cast<const float*>(eb + __builtin_popcount(d4 & (q == 8 ? ~0u : (1u << (4 * q)) - 1u)));
+      // x^(4/3) 2^(n4/4) (frame.go:187-200) as p43[x] times the band gain.
+      // Both lines of a dword at once: 4 x + 512 per 16-bit half (one
+      // v_pk_mad_u16) is the table's byte offset for x = -128..127 and >= 1024
+      // for every other |x| <= 8206 (mp3g_validate's bound); lanes holding such
+      // a line (c3: ~0.2 % of lanes, 12 % of granules have one) redo their 18
+      // lines arithmetically below, and their table reads stay inside the
+      // workgroup's LDS (offsets < 64 KiB) and are discarded.
       // Lines >= count1 hold zeros (the bitstream parse's guarantee,
       // maindata/huffman.go:130-134; mp3g_validate checks it), and requantizing
       // 0 gives 0, so long blocks need no per-line count1 test here.
       // (absent-channel lanes compute garbage that nothing reads)
+      const char* tb = reinterpret_cast<const char*>(&sh.p43[0]);
+      uint32_t big = 0;
 #pragma unroll
-      for (int j = 0; j < 18; j++) x[j] = requant_fast(xi[j], ex[j >> 1]);
+      for (int q = 0; q < 9; q++) {
+        // (v_pk_mad_u16 by hand: the compiler splits it into a shift and an
+        // add; op_sel_hi 0 on the inline constant: its high half would be 0)
+        uint32_t t;
+        asm("v_pk_mad_u16 %0, %1, 4, %2 op_sel_hi:[1,0,1]" : "=v"(t) : "v"(cw[q]), "s"(0x02000200u));
+        big |= t;
+        x[2 * q] = *reinterpret_cast<const float*>(tb + (t & 0xffffu));
+        x[2 * q + 1] = *reinterpret_cast<const float*>(tb + (t >> 16));
+      }
+#if MP3G_P43_SCHED
+      __builtin_amdgcn_sched_barrier(0);
+#endif
+#pragma unroll
+      for (int j = 0; j < 18; j++) x[j] *= gq[j >> 1];
+      if (big & 0xfc00fc00u) {
+#pragma unroll
+        for (int q = 0; q < 9; q++) {
+          x[2 * q] = requant_gain(cw[q] & 0xffffu, gq[q]);
+          x[2 * q + 1] = requant_gain(cw[q] >> 16, gq[q]);
+        }
+      }
     } else {
       int nsfs = 0;  // short bands whose first line lies below count1 (frame.go:229-255 loop bound)
 #pragma unroll
