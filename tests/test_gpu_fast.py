@@ -148,6 +148,36 @@ def test_fast_edge_cases(gpu):
     assert not so[0]["store"].any() and not so[0]["vvec"].any()
 
 
+def test_fast_requant_table_edge(gpu):
+    """Long-block lines around the edge of the fast kernel's x^(4/3) table
+    (x = -128..127; a lane holding any other value redoes its 18 lines
+    arithmetically, exec-masked): granules with table values only and granules
+    with a few lanes outside it, at gains that keep most PCM inside +-32767 --
+    within +-1 LSB of the oracle, and batch-invariant."""
+    g, c, s = synth.synth_batch(3, 40, seed=9, p_event=0.0)
+    ch = g["ch"]
+    assert not (ch["block_type"] == 2).any()
+    ch["count1"] = 576
+    ch["global_gain"] = 134
+    rng = np.random.default_rng(4)
+    inside = np.array([-128, -127, -126, -2, -1, 1, 2, 126, 127], np.int16)
+    outside = np.array([-8206, -300, -129, 128, 129, 255, 256, 8206], np.int16)
+    c[:] = 0
+    for i in range(len(g)):
+        m = rng.random(c[i].shape) < 0.05
+        c[i][m] = rng.choice(inside, size=int(m.sum()))
+        if i % 2:  # odd granules: a few lines outside the table as well
+            m = rng.random(c[i].shape) < 0.004
+            c[i][m] = rng.choice(outside, size=int(m.sum()))
+    assert gpu.validate(g, c)[0] == 0
+    want, _ = oracle.dsp_streams(g, c, s)
+    pcm, _ = gpu.decode_host(g, c, s, mode=gpu.MODE_FAST)
+    assert_close(pcm, want, "requant table edge")
+    assert (np.abs(want) > 1000).mean() > 0.2 and (np.abs(want) < 32767).mean() > 0.99
+    pcm2, _ = fast_plan(gpu, g, c, s, chunk=3)
+    assert np.array_equal(pcm2, pcm), "requant table edge: not batch-invariant"
+
+
 def test_fast_c2_full_size(gpu):
     g, c, s = synth.synth_batch(1, 10000, seed=1)
     want, _ = oracle.dsp_streams(g, c, s)
