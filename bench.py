@@ -196,21 +196,27 @@ def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle, pip
     coef_bytes = int(2 * c1.sum())
     # once more with PCIe: bitstream-derived buffers from pinned host memory
     # up, Huffman + DSP, PCM down (the host scan is timed separately above)
-    hg = torch.from_numpy(s["granules"].view(np.uint8).copy()).pin_memory()
-    hj = torch.from_numpy(s["jobs"].view(np.uint8).copy()).pin_memory()
-    hm = torch.from_numpy(s["main_data"].copy()).pin_memory()
-    hp = torch.empty(n * 1152, dtype=torch.int16).pin_memory()
-    torch.cuda.synchronize(dev)
-    t = time.perf_counter()
-    with torch.cuda.stream(stream):
-        d_g.copy_(hg, non_blocking=True)
-        d_j.copy_(hj, non_blocking=True)
-        d_m.copy_(hm, non_blocking=True)
-        huff()
-        plan.execute(d_g, d_c, d_p, stream=h)
-        hp.copy_(d_p, non_blocking=True)
-    torch.cuda.synchronize(dev)
-    pcie_s = time.perf_counter() - t
+    pin_need = s["granules"].nbytes + s["jobs"].nbytes + s["main_data"].nbytes + n * 2304
+    pcie = pin_ok(pin_need, "bitstream PCIe pass + pipelined drop-in")
+    pipelined = pipelined and pcie
+    pcie_s = float("nan")
+    hg = hj = hm = hp = None
+    if pcie:
+        hg = pin(torch.from_numpy(s["granules"].view(np.uint8).copy()))
+        hj = pin(torch.from_numpy(s["jobs"].view(np.uint8).copy()))
+        hm = pin(torch.from_numpy(s["main_data"].copy()))
+        hp = pin(torch.empty(n * 1152, dtype=torch.int16))
+        torch.cuda.synchronize(dev)
+        t = time.perf_counter()
+        with torch.cuda.stream(stream):
+            d_g.copy_(hg, non_blocking=True)
+            d_j.copy_(hj, non_blocking=True)
+            d_m.copy_(hm, non_blocking=True)
+            huff()
+            plan.execute(d_g, d_c, d_p, stream=h)
+            hp.copy_(d_p, non_blocking=True)
+        torch.cuda.synchronize(dev)
+        pcie_s = time.perf_counter() - t
     plan.close()
     # the product's pipelined drop-in, bitstream bytes in host memory -> PCM
     # in (pinned) host memory: mp3g_decode_streams_into, groups of streams
@@ -221,7 +227,7 @@ def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle, pip
     # hp holds the device leg's PCM from the PCIe pass until the call below)
     samp = np.unique(np.concatenate([np.arange(lo, min(lo + 256, n)) for lo in (0, n // 2, max(n - 256, 0))]))
     samp_w = (samp[:, None] * 1152 + np.arange(1152)[None, :]).reshape(-1)
-    dev_pcm = hp[torch.from_numpy(samp_w)].clone()
+    dev_pcm = hp[torch.from_numpy(samp_w)].clone() if pcie else None
     pipe, pipe_same = [], None
     for _ in range(2 if pipelined else 0):
         t = time.perf_counter()
@@ -232,6 +238,10 @@ def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle, pip
         assert pipe_same, "pipelined PCM differs from the device leg's"
     pipe_s = pipe[-1] if pipe else float("nan")
     mp3g.lib().mp3g_release_cached_buffers()
+    # (the device leg's PCM stays in d_p for the oracle check below)
+    pipe_first = hp.view(torch.uint8)[:1 << 20].numpy().copy() if pipe else None
+    unpin(hg, hj, hm, hp)
+    del hg, hj, hm, hp
     # the io.Reader drop-in (mp3.NewDecoder + Read, decode.go:70-80, 361-388)
     # on the first stream: read-ahead batches (host scan, then the Huffman and
     # DSP kernels with the state carried between batches), 1 MiB reads.  Twice:
@@ -249,7 +259,7 @@ def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle, pip
         while True:
             st_r, k = dec.read_full(rbuf)  # io.ReadFull: Read until 1 MiB (Read gives <= 1 frame)
             if got_bytes == 0 and cfg == "c2" and pipe:  # c2: the same stream as the pipelined leg
-                dec_same = bool(np.array_equal(rbuf[:k], hp.view(torch.uint8)[:k].numpy()))
+                dec_same = bool(np.array_equal(rbuf[:k], pipe_first[:k]))
                 assert dec_same, "Decoder PCM differs from the pipelined leg's"
             got_bytes += k
             if st_r != 0:
@@ -289,8 +299,9 @@ def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle, pip
                           "pipelined_s": round(pipe_s, 4) if pipe else None,
                           "pcm_equals_device_leg_sample": pipe_same,
                           "api": "mp3g_decode_streams_into (16 host threads, pinned PCM out)",
-                          "serial_frames_per_s": round(frames / (scan_s + pcie_s), 1),
-                          "host_scan_s": round(scan_s, 4), "h2d_huffman_dsp_d2h_s": round(pcie_s, 4),
+                          "serial_frames_per_s": round(frames / (scan_s + pcie_s), 1) if pcie else None,
+                          "host_scan_s": round(scan_s, 4), "h2d_huffman_dsp_d2h_s": round(pcie_s, 4) if pcie else None,
+                          "skipped": None if pcie else "pinned budget per rank (bench.py pinned_budget)",
                           "pcm_d2h_bytes": int(n * 2304)},
            "decoder_api": None if not pipelined else {
                            "frames_per_s": round(dec_frames / dec_s, 1), "frames": int(dec_frames),
@@ -307,10 +318,15 @@ def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle, pip
         ost, opcm = oracle.decode_all(datas[0])
         out["cpu_full_decode"] = {"frames_per_s": round(n_frames / (time.perf_counter() - t), 1), "cores": 1,
                                   "sample": "the same first stream, oracle NewDecoder + ReadAll (parse + DSP)"}
-        got = d_p.cpu().numpy()[:len(opcm) // 2]
+        # the device leg's PCM of the first stream (its granules come first in
+        # the scan's layout) against the oracle decoding that bitstream
         want = np.frombuffer(opcm, np.int16)
+        n0 = int(s["streams"][0]["n_granules"]) * 1152
+        got = d_p[:n0].cpu().numpy()
         out["max_dpcm_lsb_vs_oracle"] = int(np.abs(got.astype(np.int32) - want).max()) if ost == 0 and \
-            len(want) == n * 1152 else "oracle status %d" % ost
+            len(want) == n0 else "oracle status %d, %d vs %d samples" % (ost, len(want), n0)
+        out["oracle_parity_sample"] = "stream 0 of the device leg (%d frames) vs oracle.decode_all of its bitstream" % (
+            n0 // 2304)
     return out
 
 
@@ -612,10 +628,10 @@ def gather_leg(args, rank, world, dev, d_pcm, n_gran, mdist):
     if rank == 0:
         out = torch.empty(total // 2, dtype=torch.int16, device=coll_dev)
         if gloo:
-            out = out.pin_memory()
+            out = pin(out)
     warm = torch.zeros(1 << 16, dtype=torch.int16, device=coll_dev)
     mdist.gather_pcm(warm, dst=0)
-    host = torch.empty(n_gran * 1152, dtype=torch.int16).pin_memory() if gloo else None
+    host = pin(torch.empty(n_gran * 1152, dtype=torch.int16)) if gloo else None
     torch.cuda.synchronize(dev)
     dist.barrier()
     torch.cuda.synchronize(dev)
@@ -659,6 +675,82 @@ def dpcm(a, b):
     return int(np.abs(a.astype(np.int32) - b.astype(np.int32)).max(initial=0))
 
 
+# Host memory of the multi-rank run: every rank pins
+# its own buffers (the bitstream leg's PCIe pass and pipelined drop-in, the
+# gloo gather's staging, rank 0's gather target), so N ranks on one node pin
+# N times as much.  The stated budget per rank: PINNED_CAP_GB, or less when
+# the node's available memory shared by its local ranks is smaller
+# (MP3G_BENCH_PINNED_GB overrides); a leg whose pinned buffers would exceed
+# what is left of it is skipped and says so in the line.
+PINNED_CAP_GB = 16.0
+_pinned = {"bytes": 0, "peak": 0, "skipped": []}
+
+
+def mem_available():
+    try:
+        for ln in open("/proc/meminfo"):
+            if ln.startswith("MemAvailable:"):
+                return int(ln.split()[1]) * 1024
+    except OSError:
+        pass
+    return None
+
+
+def pinned_budget():
+    env = os.environ.get("MP3G_BENCH_PINNED_GB")
+    if env:
+        return int(float(env) * 2**30)
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
+    cap = int(PINNED_CAP_GB * 2**30)
+    avail = _pinned.get("avail0")
+    if avail:
+        cap = min(cap, avail // (2 * max(1, local_world)))
+    return cap
+
+
+def pin_ok(nbytes, leg):
+    """True when `nbytes` more pinned bytes fit this rank's budget; records the
+    skip otherwise."""
+    if _pinned["bytes"] + nbytes <= pinned_budget():
+        return True
+    _pinned["skipped"].append({"leg": leg, "bytes": int(nbytes), "pinned_before": int(_pinned["bytes"]),
+                               "budget": int(pinned_budget())})
+    return False
+
+
+def pin(t):
+    """t.pin_memory(), counted against the rank's budget."""
+    _pinned["bytes"] += t.numel() * t.element_size()
+    _pinned["peak"] = max(_pinned["peak"], _pinned["bytes"])
+    return t.pin_memory()
+
+
+def unpin(*ts):
+    for t in ts:
+        if t is not None:
+            _pinned["bytes"] -= t.numel() * t.element_size()
+
+
+def host_memory_report(world, coll_dev):
+    """Peak RSS and peak pinned bytes of this rank, max over ranks."""
+    import resource
+    import torch
+    import torch.distributed as dist
+    rss = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss * 1024
+    v = torch.tensor([float(rss), float(_pinned["peak"])], dtype=torch.float64, device=coll_dev)
+    mine = v.clone()
+    if dist.is_initialized():
+        dist.all_reduce(v, op=dist.ReduceOp.MAX)
+    return {"peak_rss_gb_rank0": round(float(mine[0]) / 1e9, 2), "peak_rss_gb_max_over_ranks": round(float(v[0]) / 1e9, 2),
+            "peak_pinned_gb_by_bench_rank0": round(float(mine[1]) / 1e9, 2),
+            "peak_pinned_gb_by_bench_max_over_ranks": round(float(v[1]) / 1e9, 2),
+            "pinned_budget_gb_per_rank": round(pinned_budget() / 1e9, 2),
+            "mem_available_gb_at_start": round((_pinned.get("avail0") or 0) / 1e9, 1),
+            "skipped_legs": _pinned["skipped"],
+            "note": "pinned = the bench's own page-locked buffers; the library's pipelined staging arena "
+                    "(host_scan.cpp) and decoder pools come on top (DESIGN.md section 13)"}
+
+
 def launch_ranks(n):
     """`bench.py --gpus N` with no launcher around it: start N ranks with
     torch.distributed.run as a CHILD process (never exec: this process must not
@@ -693,6 +785,7 @@ def check_world(gpus, environ):
 
 def main():
     args = parse()
+    _pinned["avail0"] = mem_available()
     what = check_world(args.gpus, os.environ)
     if what == "launch":
         sys.exit(launch_ranks(args.gpus))
@@ -778,7 +871,7 @@ def main():
     if not args.no_bitstream and args.config in ("c2", "c3"):
         bitstream = bitstream_leg(args.config, rank, dev, stream,
                                   mp3g.MODE_FAST if args.mode == "fast" else mp3g.MODE_EXACT,
-                                  args.steps, args.warmup, check_oracle=rank == 0 and args.config == "c2",
+                                  args.steps, args.warmup, check_oracle=rank == 0,
                                   pipelined=not args.no_pipelined, datas=datas)
 
     polyphase = None
@@ -814,6 +907,7 @@ def main():
     gather = None
     if dist.is_initialized() and not args.no_gather:
         gather = gather_leg(args, rank, world, dev, d_pcm, n_gran, mdist)
+    host_mem = host_memory_report(world, coll_dev)
 
     if rank == 0:
         kern_ms = main_res["kernel_ms"]
@@ -865,6 +959,7 @@ def main():
             out["modes"]["fast"]["hot_granules"] = hot_timed
         if hot_cliff is not None:
             out["modes"]["fast"]["hot_cliff"] = hot_cliff
+        out["host_memory"] = host_mem
         if gather is not None:
             out["gather_ms"] = gather["ms"]
             out["gather"] = gather
@@ -938,9 +1033,9 @@ def main():
             out["max_dpcm_lsb"] = out["modes"][args.mode]["max_dpcm_lsb"]
         if world == 1 and args.config == "c5":
             # end to end on this box: host parse (all cores) + H2D + decode + D2H
-            hg = torch.from_numpy(g.view(np.uint8).copy()).pin_memory()
-            hc = torch.from_numpy(c.reshape(-1).copy()).pin_memory()
-            hp = torch.empty(n_gran * 1152, dtype=torch.int16).pin_memory()
+            hg = pin(torch.from_numpy(g.view(np.uint8).copy()))
+            hc = pin(torch.from_numpy(c.reshape(-1).copy()))
+            hp = pin(torch.empty(n_gran * 1152, dtype=torch.int16))
             plan = mp3g.Plan(streams, mode=mp3g.MODE_FAST if args.mode == "fast" else mp3g.MODE_EXACT,
                              device=local)
             torch.cuda.synchronize(dev)

@@ -207,7 +207,15 @@ func (d *Decoder) Close() error {
 }
 
 // Read is io.Reader's Read (decode.go:70-80): at most the rest of one frame.
+//
+// Every method that passes d.d to the library keeps d reachable until the
+// call has returned (defer runtime.KeepAlive(d)): without it d can become
+// unreachable once d.d is loaded -- the last Read of an io.ReadAll(dec) --
+// and in reader mode the library calls back into Go during the call, where
+// a GC can run the finalizer: Close would free the decoder under the call and
+// delete the cgo.Handle its callbacks use.
 func (d *Decoder) Read(buf []byte) (int, error) {
+	defer runtime.KeepAlive(d)
 	if len(buf) == 0 {
 		return 0, nil
 	}
@@ -221,6 +229,7 @@ func (d *Decoder) Read(buf []byte) (int, error) {
 
 // ReadFull is io.ReadFull(d, buf) in one cgo call.
 func (d *Decoder) ReadFull(buf []byte) (int, error) {
+	defer runtime.KeepAlive(d)
 	if len(buf) == 0 {
 		return 0, nil
 	}
@@ -239,6 +248,7 @@ func (d *Decoder) ReadFull(buf []byte) (int, error) {
 
 // Seek is io.Seeker's Seek (decode.go:89-145), with the reference's warm-up.
 func (d *Decoder) Seek(offset int64, whence int) (int64, error) {
+	defer runtime.KeepAlive(d)
 	var np C.int64_t
 	if st := C.mp3g_decoder_seek(d.d, C.int64_t(offset), C.int(whence), &np); st != C.MP3G_OK {
 		return 0, d.statusError(st)
@@ -247,6 +257,7 @@ func (d *Decoder) Seek(offset int64, whence int) (int64, error) {
 }
 
 func (d *Decoder) info() (sr int, length, bpf, pos int64) {
+	defer runtime.KeepAlive(d)
 	var s C.int
 	var l, b, p C.int64_t
 	C.mp3g_decoder_info(d.d, &s, &l, &b, &p)
@@ -264,21 +275,48 @@ func (d *Decoder) BytesPerFrame() int64 { _, _, b, _ := d.info(); return b }
 
 // Duration, Position, Remaining, Progress, SamplePosition, SampleCount,
 // SeekToSample, Skip, SeekToTime: the time API (decode.go:232-354).
-func (d *Decoder) Duration() time.Duration { return time.Duration(C.mp3g_decoder_duration_ns(d.d)) }
-func (d *Decoder) Position() time.Duration { return time.Duration(C.mp3g_decoder_position_ns(d.d)) }
+func (d *Decoder) Duration() time.Duration {
+	defer runtime.KeepAlive(d)
+	return time.Duration(C.mp3g_decoder_duration_ns(d.d))
+}
+
+func (d *Decoder) Position() time.Duration {
+	defer runtime.KeepAlive(d)
+	return time.Duration(C.mp3g_decoder_position_ns(d.d))
+}
+
 func (d *Decoder) Remaining() time.Duration {
+	defer runtime.KeepAlive(d)
 	return time.Duration(C.mp3g_decoder_remaining_ns(d.d))
 }
-func (d *Decoder) Progress() float64     { return float64(C.mp3g_decoder_progress(d.d)) }
-func (d *Decoder) SamplePosition() int64 { return int64(C.mp3g_decoder_sample_position(d.d)) }
-func (d *Decoder) SampleCount() int64    { return int64(C.mp3g_decoder_sample_count(d.d)) }
+
+func (d *Decoder) Progress() float64 {
+	defer runtime.KeepAlive(d)
+	return float64(C.mp3g_decoder_progress(d.d))
+}
+
+func (d *Decoder) SamplePosition() int64 {
+	defer runtime.KeepAlive(d)
+	return int64(C.mp3g_decoder_sample_position(d.d))
+}
+
+func (d *Decoder) SampleCount() int64 {
+	defer runtime.KeepAlive(d)
+	return int64(C.mp3g_decoder_sample_count(d.d))
+}
+
 func (d *Decoder) SeekToSample(s int64) error {
+	defer runtime.KeepAlive(d)
 	return d.statusError(C.mp3g_decoder_seek_to_sample(d.d, C.int64_t(s)))
 }
+
 func (d *Decoder) SeekToTime(t time.Duration) error {
+	defer runtime.KeepAlive(d)
 	return d.statusError(C.mp3g_decoder_seek_to_time_ns(d.d, C.int64_t(t)))
 }
+
 func (d *Decoder) Skip(dt time.Duration) error {
+	defer runtime.KeepAlive(d)
 	return d.statusError(C.mp3g_decoder_skip_ns(d.d, C.int64_t(dt)))
 }
 
