@@ -515,12 +515,101 @@ def profiled_duration(cfg, kernel):
     return None, None, None
 
 
-def profile_check(cfg, kernel, alg_bytes):
+def profiled_cycles(cfg, kernel):
+    """Shader cycles per launch (per XCD) of the kernel in the kept profile of
+    the current set: GRBM_GUI_ACTIVE of its SQ pass (summed over the 8 XCDs by
+    rocprofv3) / 8, and the clock that profile ran at (those cycles over its
+    PMC-free duration)."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", f"{PROFILE_TAG}_{cfg}_*.json")), reverse=True):
+        d = json.load(open(f))
+        if kernel.split("::")[-1] not in d.get("kernel", ""):
+            continue
+        # preferred: the head pass's duration x the clock its own bench run
+        # measured with the probe bench.py uses here (one method on both boxes)
+        if d.get("cycles_per_launch_probe"):
+            return d["cycles_per_launch_probe"], d["head_box_clock"]["clock_ghz"], \
+                os.path.relpath(f, REPO) + " (head duration x its run's probe clock)"
+        grbm = (d.get("sq") or {}).get("GRBM_GUI_ACTIVE")
+        if grbm:
+            return grbm / 8.0, d.get("clock_ghz_est"), os.path.relpath(f, REPO) + " (GRBM_GUI_ACTIVE / 8)"
+    return None, None, None
+
+
+def fetch_calibration():
+    """What FETCH_SIZE reads for the fused kernel's own load patterns
+    (tools/fetch_calib.hip under rocprofv3, profiles/r06_fetch_calib.json):
+    `traffic` doubles FETCH_SIZE, which holds when those rows read 0.5."""
+    f = os.path.join(REPO, "profiles", "r06_fetch_calib.json")
+    if not os.path.exists(f):
+        return None
+    d = json.load(open(f))
+    r = {x["kernel"]: x["ratio"] for x in d["rows"]}
+    return {"fetch_factor": 2.0, "stream16_ratio": r.get("k_stream16"),
+            "coef_lines_12B_per_lane_ratio": r.get("k_lines12"), "descriptor_16B_ratio": r.get("k_desc"),
+            "coef_lines_to_count1_ratio": r.get("k_lines12_c1"),
+            "note": "counter / requested bytes; to-count1 rows fetch whole 128-B lines at the count1 edge "
+                    "(1.107x the requested bytes: real traffic)", "source": "profiles/r06_fetch_calib.json"}
+
+
+def profile_check(cfg, kernel, alg_bytes, box_clock=None):
+    """The roofline from the kept profile: its own duration (on the box and at
+    the clock it was taken on) and -- the box-independent form -- its cycles
+    per launch converted at the clock of the box this line was timed on
+    (clock_leg), next to the line's kernel_ms."""
     ms, src, how = profiled_duration(cfg, kernel)
     if ms is None:
         return None
-    return {"kernel_ms": round(ms, 4), "frac": round(alg_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5),
-            "source": src, "duration_source": how}
+    out = {"kernel_ms": round(ms, 4), "frac": round(alg_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5),
+           "source": src, "duration_source": how}
+    cyc, pclk, csrc = profiled_cycles(cfg, kernel)
+    if cyc is not None:
+        out.update(cycles_per_launch=round(cyc), profile_clock_ghz=round(pclk, 4) if pclk else None,
+                   cycles_source=csrc)
+        if box_clock and box_clock.get("clock_ghz"):
+            ms_box = cyc / (box_clock["clock_ghz"] * 1e9) * 1e3
+            out.update(box_clock_ghz=box_clock["clock_ghz"], kernel_ms_at_box_clock=round(ms_box, 4),
+                       frac_at_box_clock=round(alg_bytes / (ms_box * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5))
+    return out
+
+
+def clock_leg(mp3g, streams, d_g, d_c, d_pcm, mode, chunk, local, dev, launches=12):
+    """The shader clock the timed kernel runs at on this box (outside the timed
+    region): mp3g_debug_clock_probe's 8 one-wave workgroups (one per XCD)
+    spin on a side stream while `launches` launches of the timed plan run on
+    the main stream, whose last op sets the flag that ends them; clock =
+    d(s_memtime) / d(s_memrealtime) x 100 MHz, median over the probes
+    (MI355X_MICROARCH.md, DVFS item 6)."""
+    import torch
+    if not hasattr(mp3g.lib(), "mp3g_debug_clock_probe"):
+        return None
+    plan = mp3g.Plan(streams, granules_per_chunk=chunk, mode=mode, device=local)
+    main, side = torch.cuda.current_stream(dev), torch.cuda.Stream(dev)
+    flag = torch.zeros(1, dtype=torch.int32, device=dev)
+    out = torch.zeros(8 * 5, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    mp3g.clock_probe(flag, out, 8, 5000, stream=side.cuda_stream, device=local)
+    ev0.record(main)
+    for _ in range(launches):
+        plan.execute(d_g, d_c, d_pcm, stream=main.cuda_stream)
+    ev1.record(main)
+    flag.fill_(1)  # (on the main stream, after the launches)
+    torch.cuda.synchronize(dev)
+    plan.close()
+    rows = out.view(8, 5).cpu().numpy().astype(np.float64)
+    dt, dr = rows[:, 1] - rows[:, 0], rows[:, 3] - rows[:, 2]
+    ok = (rows[:, 4] != 0) & (dr > 0)
+    if not ok.any():
+        return {"clock_ghz": None, "note": "no probe saw the flag"}
+    clk = dt[ok] / dr[ok] * 0.1  # GHz: memrealtime ticks at 100 MHz
+    win_ms = float(np.median(dr[ok])) / 1e5
+    launch_ms = ev0.elapsed_time(ev1)
+    return {"clock_ghz": round(float(np.median(clk)), 4), "min_ghz": round(float(clk.min()), 4),
+            "max_ghz": round(float(clk.max()), 4), "window_ms": round(win_ms, 2),
+            "launches_ms": round(launch_ms, 2), "probes": int(ok.sum()),
+            "method": "mp3g_debug_clock_probe: d(s_memtime)/d(s_memrealtime) x 100 MHz over %d launches of the "
+                      "timed plan, median of one-wave probes on a side stream" % launches}
 
 
 def profiled_flops(cfg, kernel):
@@ -845,6 +934,11 @@ def main():
                 # (rank 0) the timed output, for the parity check below
                 "pcm": d_pcm.cpu().numpy().reshape(-1, 576, 2) if rank == 0 else None}
 
+    # the clock the headline kernel runs at on this box, measured on its own
+    # launches just before the timed region (they double as warm-up; the
+    # profile passes keep taking the last --steps launches as the timed ones)
+    box_clock = clock_leg(mp3g, streams, d_g, d_c, d_pcm,
+                          mp3g.MODE_FAST if args.mode == "fast" else mp3g.MODE_EXACT, args.chunk, local, dev)
     modes = [args.mode] + ([] if args.single_mode else [m for m in MODES if m != args.mode])
     res = {m: measure(m) for m in modes}
     main_res = res[args.mode]
@@ -937,10 +1031,13 @@ def main():
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 5),
                          "traffic": traffic, "traffic_source": traffic_src,
                          "traffic_same_build": None if traffic_sha is None else traffic_sha == lib_sha16(),
+                         "traffic_calibration": fetch_calibration(),
                          "kernel": MODES[args.mode][1], "kernel_ms": round(kern_ms, 4),
                          # the same roofline from the kept profile's kernel duration
                          # (rocprofv3 kernel trace, no counters): reproducible from profiles/
-                         "profile": profile_check(args.config, MODES[args.mode][1], n_gran * BYTES_PER_GRANULE),
+                         "profile": profile_check(args.config, MODES[args.mode][1], n_gran * BYTES_PER_GRANULE,
+                                                  box_clock),
+                         "box_clock": box_clock,
                          "algorithmic_bytes_per_frame": BYTES_PER_FRAME,
                          "algorithmic_bytes_per_launch": n_gran * BYTES_PER_GRANULE,
                          # what binds instead (DESIGN.md "Roofline"): VALU issue and

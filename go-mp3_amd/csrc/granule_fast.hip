@@ -11,10 +11,13 @@
 // (<= 128 VGPRs, 9.1 KB of LDS per wave + 4 KB shared).  A wave walks its
 // chunk granule by granule with wave-level LDS ordering only:
 //   front end   lane = (ch, sb): the 18 lines of its subband from registers
-//               (prefetched one granule ahead) -- requantize as
-//               x 2^(log2|x|/3 + n4/4), short blocks through an LDS gather
-//               (the reorder); MS pairs through v_permlane32_swap, intensity
-//               stereo per lane; antialias butterflies via DPP wave shifts;
+//               (prefetched one granule ahead) -- long blocks requantized as
+//               p43[x] * 2^(n4/4) (sign(x)|x|^(4/3) for |x| < 128 from a 1-KB
+//               LDS table times the band gain; a lane holding a larger |x|
+//               redoes its lines arithmetically), short blocks as
+//               x 2^(log2|x|/3 + n4/4) through an LDS gather (the reorder);
+//               MS pairs through v_permlane32_swap, intensity stereo per
+//               lane; antialias butterflies via DPP wave shifts;
 //   IMDCT       lane = (ch, sb): long blocks as a packed DCT-IV-18
 //               (dct4_18.h), the overlap `store` in the lane's VGPRs for the
 //               whole chunk, frequency inversion folded into window signs;
@@ -24,9 +27,14 @@
 //   window      lane = (ch, i): 16 taps (V->X signs and x32767 folded in)
 //               over operand pairs of the column-major ring, s16 (L, R) pairs
 //               through one v_permlane32_swap per slot pair, stored at once.
-// Hot granules (hybrid output above kHotS) run the same stages in the
-// reference's operation order (the *_exact functions) after a rewind of the
-// wave to the granule's replay start: PCM within +-1 LSB on every valid input.
+// Hot granules (hybrid output above the magnitude bound kHotS / kHotL1) are
+// not redone here: the wave records their zones (the granules whose PCM
+// depends on them) and appends them to the launch's zone list, and a second
+// launch -- the exact v4 kernel over the list (kernels_fast.hip launch_fast)
+// -- decodes every zone in the reference's operation order from its replay
+// start and overwrites its PCM: within +-1 LSB on every valid input.  (The
+// in-wave pass with the *_exact functions is compiled into the diagnostic
+// kStamp build only.)
 // (compiled in its own TU, kernels_fast.hip)
 #pragma clang fp contract(fast)
 #include <type_traits>
@@ -1752,7 +1760,12 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       z.reserved = 0;
       zone_list[base + zl] = z;
     }
-    if constexpr (kHotCount) {
+  }
+  // (counting build) a chunk counts its flagged granules even when none of
+  // them recorded a zone -- a replayed granule whose V feeds no output is
+  // hot all the same (counter [2] is every hot granule the fast pass met)
+  if constexpr (!kStamp && kHotCount) {
+    if (nz || n_flagged) {
       uint32_t n_out = 0;
       for (uint32_t i = 0; i < nz; i++)
         n_out += __builtin_amdgcn_readfirstlane(s.zone[i][1]) - __builtin_amdgcn_readfirstlane(s.zone[i][0]);

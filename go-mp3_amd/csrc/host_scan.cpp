@@ -620,16 +620,6 @@ int mp3g_decode_streams_into(int device, uint32_t n_streams, const uint8_t* cons
     }
     if (rc == MP3G_OK && !B->d_coef.reserve(max_ng * MP3G_COEF_PER_GRANULE * sizeof(int16_t)))
       rc = abi_fail(MP3G_ERR_DEVICE, "decode_streams_into: buffers");
-    // (a group's plan has at most one chunk per granule: max_ng chunks)
-    const uint64_t zone_cap = (uint64_t)kZoneListPerChunk * std::max<uint64_t>(8, max_ng);
-    if (rc == MP3G_OK && zone_cap > 0xffffffffu) rc = abi_fail(MP3G_ERR_UNSUPPORTED, "decode_streams_into: group too large");
-    if (rc == MP3G_OK && B->zone_cap < zone_cap) {
-      if (!B->d_zones.reserve(zone_scratch_bytes((uint32_t)zone_cap)) ||
-          zone_scratch_init(B->d_zones.p, (uint32_t)zone_cap) != hipSuccess)
-        rc = abi_fail(MP3G_ERR_DEVICE, "decode_streams_into: buffers");
-      else
-        B->zone_cap = (uint32_t)zone_cap;
-    }
     trace.mark("buffers");
     hipStream_t up = B->up, comp = B->comp, down = B->down;
     // the caller's PCM buffer: pinned and 16-B aligned -> our copy kernel
@@ -699,6 +689,27 @@ int mp3g_decode_streams_into(int device, uint32_t n_streams, const uint8_t* cons
         break;
       }
       if (!chunks.empty()) std::memcpy(h_chunks, chunks.data(), chunks.size() * sizeof(ChunkDesc));
+      // the fast kernel's zone scratch: kZoneListPerChunk zones per chunk of
+      // this group's plan (the cost model keeps chunks far fewer than
+      // granules), grown on demand -- after the kernels that use the old one
+      // are done (the scratch is shared by every group on `comp`)
+      if ((mode & 0xffu) == MP3G_MODE_FAST) {
+        const uint64_t zone_cap = (uint64_t)kZoneListPerChunk * std::max<uint64_t>(8, chunks.size());
+        if (zone_cap > 0xffffffffu) {
+          rc = abi_fail(MP3G_ERR_UNSUPPORTED, "decode_streams_into: group too large");
+          break;
+        }
+        if (B->zone_cap < zone_cap) {
+          const uint64_t grow = std::max<uint64_t>(zone_cap, (uint64_t)B->zone_cap * 2);
+          const uint32_t cap = (uint32_t)std::min<uint64_t>(grow, 0xffffffffu);
+          if (hipStreamSynchronize(B->comp) != hipSuccess || !B->d_zones.reserve(zone_scratch_bytes(cap)) ||
+              zone_scratch_init(B->d_zones.p, cap) != hipSuccess) {
+            rc = abi_fail(MP3G_ERR_DEVICE, "decode_streams_into: buffers");
+            break;
+          }
+          B->zone_cap = cap;
+        }
+      }
       const uint32_t stage = mp3g_huffman_stage_flags(jobs, ng);
       // up
       hipError_t e = gi >= 2 ? hipStreamWaitEvent(up, B->kern[slot], 0) : hipSuccess;

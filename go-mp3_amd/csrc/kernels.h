@@ -73,6 +73,9 @@ constexpr int kHotCounters = 4;
 // memory to device-accessible pinned host memory (`dst`: its device address)
 // by a kernel of `blocks` 256-thread workgroups (kernels.hip).
 hipError_t launch_copy_out(const void* d_src, void* dst, size_t bytes, int blocks, hipStream_t stream);
+// diagnostic: shader clock under load (mp3g_debug_clock_probe)
+hipError_t launch_clock_probe(const uint32_t* d_flag, unsigned long long* d_out, uint32_t n_waves,
+                              unsigned long long max_ticks, hipStream_t stream);
 
 // Chunks of `variant` resident per CU (one per wave for the fast kernel, one
 // per workgroup for the exact kernels), from the kernel's VGPR / LDS usage.

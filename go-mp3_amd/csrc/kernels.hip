@@ -65,6 +65,40 @@ hipError_t launch_copy_out(const void* d_src, void* dst, size_t bytes, int block
   return hipGetLastError();
 }
 
+// Shader clock under load (diagnostic, mp3g_debug_clock_probe): one wave per
+// workgroup spins beside whatever the device runs until *flag turns non-zero
+// (or max_ticks of the 100 MHz real-time counter pass) and reports its
+// s_memtime (shader cycles) and s_memrealtime at both ends of the window:
+// clock = d(memtime) / d(memrealtime) x 100 MHz (MI355X_MICROARCH.md, DVFS
+// item 6).  Lane 0 stores four dwords pairs per workgroup with vector stores.
+__global__ void __launch_bounds__(64) clock_probe_kernel(const uint32_t* flag, unsigned long long* out,
+                                                         unsigned long long max_ticks) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  unsigned long long r = r0;
+  uint32_t seen = 0;
+  while (r - r0 < max_ticks) {
+    seen = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (seen) break;
+    __builtin_amdgcn_s_sleep(8);
+    r = __builtin_amdgcn_s_memrealtime();
+  }
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) {
+    unsigned long long* o = out + 5 * blockIdx.x;
+    o[0] = t0;
+    o[1] = t1;
+    o[2] = r0;
+    o[3] = r1;
+    o[4] = seen;
+  }
+}
+
+hipError_t launch_clock_probe(const uint32_t* d_flag, unsigned long long* d_out, uint32_t n_waves,
+                              unsigned long long max_ticks, hipStream_t stream) {
+  hipLaunchKernelGGL(clock_probe_kernel, dim3(n_waves), dim3(64), 0, stream, d_flag, d_out, max_ticks);
+  return hipGetLastError();
+}
+
 int chunks_per_cu(int variant) {
   hipFuncAttributes a;
   hipError_t e;

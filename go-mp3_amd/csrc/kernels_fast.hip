@@ -83,7 +83,13 @@ hipError_t launch_fast(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_
   hipLaunchKernelGGL(v4::granule_wexact_kernel<true>, dim3(blocks), dim3(64 * v4::kXWaves), 0, stream,
                      reinterpret_cast<const ChunkDesc*>(aux + 8), zones->cap, d_gran, d_coef, d_state_in,
                      d_state_out, d_pcm, aux);
-  return hipGetLastError();
+  e = hipGetLastError();
+  // the fast kernel ran (or will) and may have listed zones that no zone
+  // launch will empty: reset the count and done words behind it on the
+  // stream, so that the next launch does not decode stale zones into its own
+  // buffers (the error is returned either way)
+  if (e != hipSuccess) (void)hipMemsetAsync(aux, 0, 2 * sizeof(uint32_t), stream);
+  return e;
 }
 
 hipError_t wexact_kernel_attributes(hipFuncAttributes* a, int* waves_per_block) {

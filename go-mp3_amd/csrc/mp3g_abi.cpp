@@ -567,6 +567,18 @@ int mp3g_plan_debug_timeline(mp3g_plan* p, const mp3g_granule* d_gran, const int
   return MP3G_OK;
 }
 
+int mp3g_debug_clock_probe(int device, const uint32_t* d_flag, uint64_t* d_out, uint32_t n_waves,
+                           uint32_t max_ms, void* hip_stream) {
+  if (!d_flag || !d_out || n_waves == 0 || n_waves > 1024 || max_ms == 0 || max_ms > 10000)
+    return fail(MP3G_ERR_INVALID_ARGUMENT, "clock probe arguments");
+  DeviceGuard guard(device);
+  if (guard.err != hipSuccess) return fail(MP3G_ERR_NO_DEVICE, "hipSetDevice", guard.err);
+  const hipError_t e = launch_clock_probe(d_flag, reinterpret_cast<unsigned long long*>(d_out), n_waves,
+                                          100000ull * max_ms, static_cast<hipStream_t>(hip_stream));
+  if (e != hipSuccess) return fail(MP3G_ERR_DEVICE, "clock probe launch", e);
+  return MP3G_OK;
+}
+
 int mp3g_decode_host(int device, const mp3g_granule* granules, const int16_t* coeffs,
                      uint64_t n_granules, const mp3g_stream* streams, uint32_t n_streams,
                      const mp3g_state* state_in, mp3g_state* state_out, int16_t* pcm,

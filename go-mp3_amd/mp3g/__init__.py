@@ -98,6 +98,8 @@ def lib():
         L.mp3g_decode_host.argtypes = [C.c_int, vp, vp, u64, vp, u32, vp, vp, vp, u32]
         L.mp3g_plan_debug_phases.argtypes = [vp, vp, vp, vp, C.POINTER(u64), vp]
         L.mp3g_plan_debug_timeline.argtypes = [vp, vp, vp, vp, C.POINTER(u64), vp]
+        if hasattr(L, "mp3g_debug_clock_probe"):  # (an older build through MP3G_LIB: A/B runs)
+            L.mp3g_debug_clock_probe.argtypes = [C.c_int, vp, vp, u32, u32, vp]
         i64, sz = C.c_int64, C.c_size_t
         L.mp3g_parse_stream.argtypes = [vp, sz, C.POINTER(vp), C.POINTER(vp), C.POINTER(u64),
                                         C.POINTER(C.c_int)]
@@ -451,6 +453,19 @@ def decode_streams_into(datas, out, mode=MODE_EXACT, n_threads=0, n_groups=0, de
     _check(lib().mp3g_decode_streams_into(device, len(datas), ptrs, lens, n_threads, mode, n_groups,
                                           C.c_void_p(ptr), cap, C.byref(n), _ptr(streams), _ptr(status)))
     return n.value, streams, status[:len(datas)]
+
+
+def clock_probe(d_flag, d_out, n_waves=8, max_ms=5000, stream=None, device=0):
+    """mp3g_debug_clock_probe (diagnostic): n_waves one-wave workgroups spin on
+    `stream` until the int32 device word d_flag turns non-zero (or max_ms
+    pass), writing (s_memtime, s_memtime, s_memrealtime, s_memrealtime, seen)
+    at both ends of their window into the int64 device tensor d_out
+    (5 x n_waves).  Asynchronous: set the flag from another stream after the
+    work whose clock is measured."""
+    if d_out.numel() < 5 * n_waves or d_out.element_size() != 8 or d_flag.element_size() != 4:
+        raise ValueError("clock_probe: d_out needs 5 x n_waves int64, d_flag one int32")
+    _check(lib().mp3g_debug_clock_probe(device, C.c_void_p(d_flag.data_ptr()), C.c_void_p(d_out.data_ptr()),
+                                        n_waves, max_ms, C.c_void_p(stream or 0)))
 
 
 class Decoder:

@@ -19,6 +19,10 @@
  *
  * Threading: a context / plan is single-threaded like mp3.Decoder
  * (reference decode.go:27-33); distinct contexts may be used concurrently.
+ * Executions of one fast-mode plan (mp3g_plan_execute) must also be ordered
+ * on the device: one stream, or streams synchronised between them -- its
+ * launches share the plan's zone list (ABI 5).  One plan per stream for
+ * concurrent launches.
  */
 #ifndef MP3G_H
 #define MP3G_H
@@ -39,7 +43,8 @@ extern "C" {
  *    MP3G_HUFF_STAGE_WIDE flags of mp3g_huffman_execute_ex and the advice
  *    mp3g_huffman_stage_flags.
  * 5: mp3g_plan_hot_stats and MP3G_FLAG_HOT_STATS (the fast kernel's
- *    hot-granule fallback counters). */
+ *    hot-granule fallback counters); a fast-mode plan owns a zone list its
+ *    launches share, so executions of one plan must be stream-ordered. */
 #define MP3G_ABI_VERSION 5
 
 /* ---- status codes ------------------------------------------------------ */
@@ -183,7 +188,13 @@ int mp3g_plan_info(const mp3g_plan* plan, uint64_t* n_chunks, uint64_t* n_granul
 
 /* Asynchronous execution on device-resident buffers.  All pointers are device
  * pointers; `hip_stream` is a hipStream_t (NULL = default stream).  state_in /
- * state_out may be NULL when no stream of the plan uses the flag. */
+ * state_out may be NULL when no stream of the plan uses the flag.
+ * Fast mode (ABI 5): a launch's hot zones go through a zone list owned by the
+ * plan and emptied by the launch itself (graph replays are fine), so two
+ * executions of ONE plan must not overlap on the device -- issue them on one
+ * stream or synchronise the streams; concurrent launches need a plan each.
+ * If the zone launch cannot be enqueued, the list is reset on the stream
+ * before the error is returned (the next execution starts clean). */
 int mp3g_plan_execute(mp3g_plan* plan, const mp3g_granule* d_granules,
                       const int16_t* d_coeffs, const mp3g_state* d_state_in,
                       mp3g_state* d_state_out, int16_t* d_pcm, void* hip_stream);
@@ -437,6 +448,15 @@ int mp3g_plan_debug_phases(mp3g_plan* plan, const mp3g_granule* d_granules, cons
  * its granule loop and at exit: the launch's ramp, per-wave span and tail. */
 int mp3g_plan_debug_timeline(mp3g_plan* plan, const mp3g_granule* d_granules, const int16_t* d_coeffs,
                              int16_t* d_pcm, uint64_t* out_ticks, void* hip_stream);
+
+/* Shader clock under load: launches n_waves one-wave workgroups on
+ * hip_stream that spin until the device word *d_flag turns non-zero (set it
+ * from another stream after the work to be measured) or max_ms (<= 10,000)
+ * pass, each writing 5 uint64 to d_out[5 * wg ..]: s_memtime (shader cycles)
+ * and s_memrealtime (100 MHz) at the start and the end of its window, and
+ * whether it saw the flag.  Asynchronous. */
+int mp3g_debug_clock_probe(int device, const uint32_t* d_flag, uint64_t* d_out, uint32_t n_waves,
+                           uint32_t max_ms, void* hip_stream);
 
 /* ---- Xing / Info / LAME tag (lameinfo/lameinfo.go) ----
  * The reference's lameinfo package: the tag in the first frame (encoder delay

@@ -91,6 +91,30 @@ def calibration(src, tag, dst):
     return res
 
 
+def head_box_clock(src, tag, cfg):
+    """The shader clock the head pass's own bench run measured (bench.py
+    clock_leg, before its timed launches): its JSON line in the pass's
+    section of prof_<tag>.log, or None."""
+    f = os.path.join(src, f"prof_{tag}.log")
+    if not os.path.exists(f):
+        return None
+    sec, inside = [], False
+    for ln in open(f, errors="replace"):
+        if ln.startswith(f"== head_{cfg}:"):
+            sec, inside = [], True
+        elif ln.startswith(f"== head_{cfg} rc="):
+            inside = False
+        elif inside:
+            sec.append(ln)
+    for ln in reversed(sec):
+        if ln.startswith('{"metric"'):
+            try:
+                return (json.loads(ln).get("roofline") or {}).get("box_clock")
+            except ValueError:
+                return None
+    return None
+
+
 def main(src, tag, cfg, dst="profiles", bytes_per_launch=None, kernel=None, suffix=""):
     kernel = kernel or KERNEL
     base = os.path.join(src, f"prof_{tag}_{cfg}")
@@ -124,10 +148,20 @@ def main(src, tag, cfg, dst="profiles", bytes_per_launch=None, kernel=None, suff
     else:
         avg_ns = float(k["AverageNs"])
         out.update(calls=int(k["Calls"]), avg_ns=avg_ns, min_ns=float(k["MinNs"]), max_ns=float(k["MaxNs"]))
+    clk = head_box_clock(src, tag, cfg) if dur_src == "head" else None
+    if clk and clk.get("clock_ghz"):
+        # cycles per launch at the clock the head pass ran at, measured the way
+        # bench.py measures the clock of the box it times (s_memtime over
+        # s_memrealtime): the box-independent form of the kept duration
+        out.update(head_box_clock=clk, cycles_per_launch_probe=avg_ns * clk["clock_ghz"])
     if fetch is not None and write is not None:
+        # FETCH_SIZE x 2: calibrated for this kernel's own load patterns by
+        # tools/fetch_calib.hip (profiles/r06_fetch_calib.json: the 12-B-per-lane
+        # coefficient loads and the 16-B descriptor loads read exactly 0.5 of
+        # their bytes, as the guide's 16-B streaming reads)
         hbm = (2 * fetch + write) * 1024
         out.update(fetch_kib=fetch, write_kib=write, hbm_bytes_per_launch_corrected=hbm,
-                   hbm_gbps=hbm / avg_ns)
+                   hbm_gbps=hbm / avg_ns, fetch_factor=2.0, fetch_calibration="profiles/r06_fetch_calib.json")
     if sq:
         out["sq"] = sq
         if "GRBM_GUI_ACTIVE" in sq:
