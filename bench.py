@@ -457,7 +457,20 @@ def polyphase_leg(args, rank, dev, stream, d_g, streams, n_gran, local):
     return out
 
 
-PROFILE_TAG = "r05"  # profiles/<tag>_<cfg>_<kernel>.json of the current kernels
+def _profile_tag():
+    """profiles/<tag>_<cfg>_<kernel>.json of the current kernels: the newest
+    round tag with a kept fused-kernel profile (MP3G_PROFILE_TAG overrides)."""
+    import glob
+    import re
+    if os.environ.get("MP3G_PROFILE_TAG"):
+        return os.environ["MP3G_PROFILE_TAG"]
+    tags = [re.match(r"(r\d+)_c3_granule_fast_kernel\.json$", os.path.basename(f))
+            for f in glob.glob(os.path.join(REPO, "profiles", "r*_c3_granule_fast_kernel.json"))]
+    tags = sorted(m.group(1) for m in tags if m)
+    return tags[-1] if tags else "r05"
+
+
+PROFILE_TAG = _profile_tag()
 
 
 def profiled_issue(cfg, kernel):
@@ -716,11 +729,16 @@ def gather_leg(args, rank, world, dev, d_pcm, n_gran, mdist):
     out = None
     if rank == 0:
         out = torch.empty(total // 2, dtype=torch.int16, device=coll_dev)
-        if gloo:
+        # (gloo reads pageable memory too: pinned only within the rank's budget)
+        if gloo and pin_ok(total, "gloo gather target pinned (pageable instead)"):
             out = pin(out)
     warm = torch.zeros(1 << 16, dtype=torch.int16, device=coll_dev)
     mdist.gather_pcm(warm, dst=0)
-    host = pin(torch.empty(n_gran * 1152, dtype=torch.int16)) if gloo else None
+    host = None
+    if gloo:
+        host = torch.empty(n_gran * 1152, dtype=torch.int16)
+        if pin_ok(n_gran * 2304, "gloo gather staging pinned (pageable instead)"):
+            host = pin(host)
     torch.cuda.synchronize(dev)
     dist.barrier()
     torch.cuda.synchronize(dev)

@@ -57,6 +57,16 @@ namespace v3 {
 #ifndef MP3G_FAST_PRIO
 #define MP3G_FAST_PRIO 1  // progress-balanced s_setprio (0: A/B experiments)
 #endif
+// The granule descriptors one dword per lane in a VGPR (lane i < 40 holds
+// dword i of the 160-B mp3g_granule), loaded one granule ahead by a single
+// buffer load: the header and channel words come out by v_readlane, the long
+// bands' scale factors by ds_bpermute -- no LDS round trip and no LDS copy of
+// the next descriptors per granule.  The rare paths that index the scale
+// factors per line (short blocks, intensity stereo) first drop the descriptor
+// into the wave's LDS slot.  0: the descriptors staged in LDS (round 5).
+#ifndef MP3G_FAST_DESC_VGPR
+#define MP3G_FAST_DESC_VGPR 1
+#endif
 #ifndef MP3G_FAST_WG_WAVES
 #define MP3G_FAST_WG_WAVES 8
 #endif
@@ -105,6 +115,9 @@ constexpr int kHist = 16;
 #endif
 constexpr int kSlots = kHist + 18;
 static_assert(kSlots == kFastRingSlots, "FastTables::sinfo indexes the staged ring");
+#ifndef MP3G_FAST_P43
+#define MP3G_FAST_P43 1  // long-block requantize through the p43 LDS table (0: arithmetic, A/B)
+#endif
 #ifndef MP3G_P43_SCHED
 #define MP3G_P43_SCHED 0
 #endif
@@ -214,6 +227,25 @@ __device__ __forceinline__ void load_lines_lim(const int16_t* coef, uint32_t g, 
     cw[3 * i + 2] = v[2];
   }
 }
+// Lane i < 40: dword i of granule g's descriptor (0 on the other lanes, and
+// everywhere when !valid: a resource without records).
+__device__ __forceinline__ uint32_t load_desc_dword(const mp3g_granule* gran, uint32_t g, int lane, bool valid) {
+  const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<mp3g_granule*>(gran + g), (short)0, valid ? (int)sizeof(mp3g_granule) : 0, 0x00020000);
+  return __builtin_amdgcn_raw_buffer_load_b32(rd, 4 * lane, 0, 0);
+}
+// dword k of a descriptor held one dword per lane (wave-uniform k): an SGPR
+__device__ __forceinline__ uint32_t desc_word(uint32_t dv, int k) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)dv, k);
+}
+// byte b of a descriptor held one dword per lane, per lane (b may differ by lane)
+__device__ __forceinline__ uint32_t desc_byte(uint32_t dv, int b) {
+  return ((uint32_t)__builtin_amdgcn_ds_bpermute((b >> 2) << 2, (int)dv) >> (8 * (b & 3))) & 0xffu;
+}
+static_assert(sizeof(mp3g_granule) == 160 && offsetof(mp3g_granule, ch) == 8 && sizeof(mp3g_channel) == 72 &&
+                  offsetof(mp3g_channel, scalefac_l) == 11,
+              "descriptor dword layout");
+
 // the line limit of lane (ch, sb) in granule g (wave-uniform g: scalar loads)
 __device__ __forceinline__ int count1_lim(const mp3g_granule* gran, uint32_t g, int lane) {
   const uint32_t h = gran[g].header;
@@ -1141,12 +1173,22 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
   }
 
   uint32_t cw[9] = {};  // the current granule's raw coefficients (lane's 18 lines)
+#if MP3G_FAST_DESC_VGPR
+  // the descriptors of the current and the next granule, one dword per lane
+  uint32_t dv = 0, dvn = 0;
+  if (w < end) {
+    load_lines_lim(coef, w, lane, cw, (int)(MP3G_COEF_PER_GRANULE * sizeof(int16_t)), count1_lim(gran, w, lane));
+    dv = load_desc_dword(gran, w, lane, true);
+    dvn = load_desc_dword(gran, w + 1, lane, w + 1 < end);
+  }
+#else
   if (w < end) {
     load_lines_lim(coef, w, lane, cw, (int)(MP3G_COEF_PER_GRANULE * sizeof(int16_t)), count1_lim(gran, w, lane));
     if (lane < 10) reinterpret_cast<uint4*>(&s.desc)[lane] = reinterpret_cast<const uint4*>(gran + w)[lane];
     if (lane < 10 && w + 1 < end)
       reinterpret_cast<uint4*>(&s.descn)[lane] = reinterpret_cast<const uint4*>(gran + w + 1)[lane];
   }
+#endif
   shared_init();
   __syncthreads();  // the only workgroup barrier: the waves are independent from here on
 
@@ -1253,10 +1295,16 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     // the header and both channels' parameters in one LDS round trip, before
     // anything branches on them (read under the halo test first, the header
     // took a round trip of its own: c3 +0.7 %)
+#if MP3G_FAST_DESC_VGPR
+    // header (dword 0) and the channels' first two dwords (2, 3 and 20, 21)
+    // straight from the lanes that hold them
+    const uint32_t h = desc_word(dv, 0);
+#else
     const uint32_t hv = s.desc.header;
     const uint2 cv0 = *reinterpret_cast<const uint2*>(&s.desc.ch[0]);
     const uint2 cv1 = *reinterpret_cast<const uint2*>(&s.desc.ch[1]);
     const uint32_t h = __builtin_amdgcn_readfirstlane(hv);
+#endif
     // does a replayed granule's V feed anything? (see v2 / DESIGN.md halo)
     bool need_v = true;
     if (!out && g + 1 < out_first) need_v = hdr_nch(gran[g + 1].header) < hdr_nch(h);
@@ -1265,11 +1313,25 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     // the channels' scalar parameters in SGPRs:
     // dword 0 = count1 | global_gain << 16 | scalefac_scale << 24,
     // dword 1 = preflag | win_switch_flag << 8 | block_type << 16 | mixed_block_flag << 24
+#if MP3G_FAST_DESC_VGPR
+    const uint32_t cp0[2] = {desc_word(dv, 2), desc_word(dv, 20)};
+    const uint32_t cp1[2] = {desc_word(dv, 3), desc_word(dv, 21)};
+#else
     const uint32_t cp0[2] = {(uint32_t)__builtin_amdgcn_readfirstlane(cv0.x), (uint32_t)__builtin_amdgcn_readfirstlane(cv1.x)};
     const uint32_t cp1[2] = {(uint32_t)__builtin_amdgcn_readfirstlane(cv0.y), (uint32_t)__builtin_amdgcn_readfirstlane(cv1.y)};
+#endif
     auto is_short = [](uint32_t d1) { return (d1 & 0x00ffff00u) == 0x00020100u; };  // win_switch 1, block_type 2
     // wave-uniform: every channel of this granule is a long block (no reorder)
     const bool all_long = !is_short(cp1[0]) && (nch == 1 || !is_short(cp1[1]));
+#if MP3G_FAST_DESC_VGPR
+    // the rare paths that index scale factors per line read the descriptor
+    // from the wave's LDS slot: short blocks and intensity stereo
+    if (!all_long || (nch == 2 && hdr_mode(h) == 1 && (h & 0x10u))) {
+      const int l = lane_fresh();
+      if (l < 40) reinterpret_cast<uint32_t*>(&s.desc)[l] = dv;
+      wave_sync();
+    }
+#endif
     // this lane's channel (lanes of an absent channel mirror channel 0's block
     // layout: no extra divergence)
     const uint32_t d0 = (act && ch) ? cp0[1] : cp0[0], d1 = (act && ch) ? cp1[1] : cp1[0];
@@ -1280,10 +1342,17 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       // long bands: lane = (ch, sfb = k), k < 22 -- the lane's own channel
       // parameters d0 / d1 (an absent channel's lanes write values nothing reads)
       const int e = lane_fresh();
+#if MP3G_FAST_DESC_VGPR
+      // scalefac_l[sfb] of channel ch: descriptor byte 19 + 72 ch + sfb
+      // (every lane takes part in the permute: lanes >= 22 read bytes they drop)
+      const int sfl_byte = (int)desc_byte(dv, 19 + 72 * ch + (e & 31));
+#else
+      const int sfl_byte = (int)s.desc.ch[ch].scalefac_l[e & 31];
+#endif
       if ((e & 31) < 22) {
         const int sfb = e & 31;
         const int v = (int)((d0 >> 16) & 0xffu) - 210 -
-                      ((d0 >> 24) ? 4 : 2) * ((int)s.desc.ch[ch].scalefac_l[sfb] + (int)(d1 & 0xffu) * kPretab(sfb));
+                      ((d0 >> 24) ? 4 : 2) * (sfl_byte + (int)(d1 & 0xffu) * kPretab(sfb));
         if (all_long) s.expo_gain()[22 * ch + sfb] = __builtin_amdgcn_exp2f(0.25f * (float)v);
         else s.expo[22 * ch + sfb] = (_Float16)(0.25f * (float)v);
       }
@@ -1332,6 +1401,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       // maindata/huffman.go:130-134; mp3g_validate checks it), and requantizing
       // 0 gives 0, so long blocks need no per-line count1 test here.
       // (absent-channel lanes compute garbage that nothing reads)
+#if MP3G_FAST_P43
       const char* tb = reinterpret_cast<const char*>(&sh.p43[0]);
       uint32_t big = 0;
 #pragma unroll
@@ -1356,6 +1426,13 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
           x[2 * q + 1] = requant_gain(cw[q] >> 16, gq[q]);
         }
       }
+#else  // (A/B: every long-block line arithmetically, the round-5 path before the table)
+#pragma unroll
+      for (int q = 0; q < 9; q++) {
+        x[2 * q] = requant_gain(cw[q] & 0xffffu, gq[q]);
+        x[2 * q + 1] = requant_gain(cw[q] >> 16, gq[q]);
+      }
+#endif
     } else {
       int nsfs = 0;  // short bands whose first line lies below count1 (frame.go:229-255 loop bound)
 #pragma unroll
@@ -1609,7 +1686,11 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     // reload costs an s_waitcnt vmcnt(0), which would also wait for this
     // prefetch
     const bool more = g + 1 < end;
+#if MP3G_FAST_DESC_VGPR
+    uint32_t pdw;  // the descriptor two granules ahead, one dword per lane
+#else
     uint4 pd = {0, 0, 0, 0};
+#endif
     // issued unconditionally (straight-line vmcnt accounting, as the PCM
     // stores below): past the chunk the resources have no records
     {
@@ -1617,14 +1698,23 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       // earlier): its count1s bound this prefetch; the descriptor two ahead
       // is loaded with it
       {
+#if MP3G_FAST_DESC_VGPR
+        const uint32_t nh = desc_word(dvn, 0);
+        const int c0 = (int)(desc_word(dvn, 2) & 0xffffu);
+        const int c1 = (int)(desc_word(dvn, 20) & 0xffffu);
+#else
         const uint32_t nh = __builtin_amdgcn_readfirstlane(s.descn.header);
         const uint2 n0 = *reinterpret_cast<const uint2*>(&s.descn.ch[0]);
         const uint2 n1 = *reinterpret_cast<const uint2*>(&s.descn.ch[1]);
         const int c0 = (int)(__builtin_amdgcn_readfirstlane(n0.x) & 0xffffu);
         const int c1 = (int)(__builtin_amdgcn_readfirstlane(n1.x) & 0xffffu);
+#endif
         const int lim = ch ? (hdr_nch(nh) == 2 ? c1 : 0) : c0;
         load_lines_lim(coef, g + 1, lane, cw, more ? (int)(MP3G_COEF_PER_GRANULE * sizeof(int16_t)) : 0, lim);
       }
+#if MP3G_FAST_DESC_VGPR
+      pdw = load_desc_dword(gran, g + 2, lane_fresh(), g + 2 < end);
+#else
       if (lane < 10) {
         const bool more2 = g + 2 < end;
         const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
@@ -1632,6 +1722,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
         const auto v = __builtin_amdgcn_raw_buffer_load_b128(rd, lane * 16, 0, 0);
         pd = make_uint4(v[0], v[1], v[2], v[3]);
       }
+#endif
     }
 
     // ---- matrixing (frame.go:642-648): S rows into the ring (lane (ch, sb)
@@ -1676,6 +1767,10 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     //      for the stores too ----
     // (lane recomputed: the two LDS addresses kept live across the granule
     // were spilled, and a scratch reload here waits for the PCM stores)
+#if MP3G_FAST_DESC_VGPR
+    dv = dvn;
+    dvn = pdw;
+#else
     if (more) {
       const int l = lane_fresh();
       if (l < 10) {
@@ -1683,6 +1778,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
         reinterpret_cast<uint4*>(&s.descn)[l] = pd;
       }
     }
+#endif
 
     window_store(g, out, nch);
     wave_sync();  // ring reads done
