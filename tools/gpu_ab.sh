@@ -40,8 +40,10 @@ import json, sys
 d = json.loads(sys.stdin.read())
 b = d.get('bitstream') or {}
 x = (d.get('modes') or {}).get('exact') or {}
+clk = (d['roofline'].get('box_clock') or {}).get('clock_ghz')
 print('$cfg', '$lib', d['value'], d['roofline']['kernel_ms'], b.get('huffman_plus_dsp_ms', '-'), d.get('max_dpcm_lsb'),
-      'exact', x.get('kernel_ms', '-'), x.get('max_dpcm_lsb', '-'))"
+      'exact', x.get('kernel_ms', '-'), x.get('max_dpcm_lsb', '-'), 'clock', clk,
+      'Mcycles', round(d['roofline']['kernel_ms'] * clk * 1e3, 3) if clk else '-')"
     done
   done
 done
