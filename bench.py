@@ -330,6 +330,62 @@ def bitstream_leg(cfg, rank, dev, stream, mode, steps, warmup, check_oracle, pip
     return out
 
 
+def real_loud_leg(args, rank, dev, stream, local, copies=64, boosts=(0, 4, 8, 12, 16, 24)):
+    """The fast mode's magnitude bound on REAL content:
+    the reference's two sample files (c5: classic_lame.mp3, mpeg2.mp3, peak
+    PCM about -6 dBFS) made louder by raising every granule's global_gain by
+    `boost` steps of 1.5 dB (the same quantised lines: a master that is louder
+    by 1.5 dB x boost, from full scale at +4 to heavily clipped), `copies` of
+    each.  Per boost: the share of PCM samples at the clip limit (oracle),
+    hot granules and the rewritten share (the counting build), the fast plan's
+    launch time, and max |dPCM| against the oracle on one copy of each file."""
+    import torch
+    import mp3g
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle  # checker of the PCM and the clip share only
+    gold = os.path.join(REPO, "tests", "golden")
+    datas = [open(os.path.join(gold, f), "rb").read() for f in ("classic_lame.mp3", "mpeg2.mp3")]
+    g0, c0, s0, st = mp3g.parse_streams(datas * copies, n_threads=16)
+    assert all(x == 7 for x in st)
+    n = len(g0)
+    n_chk = int(s0["n_granules"][0]) + int(s0["n_granules"][1])  # one copy of each file
+    h = stream.cuda_stream
+    d_c = torch.from_numpy(c0.reshape(-1).copy()).to(dev)
+    d_p = torch.empty(n * 1152, dtype=torch.int16, device=dev)
+    out = []
+    for b in boosts:
+        g2 = g0.copy()
+        g2["ch"]["global_gain"] = np.minimum(g0["ch"]["global_gain"].astype(np.int32) + b, 255).astype(np.uint8)
+        d_g = torch.from_numpy(g2.view(np.uint8).copy()).to(dev)
+        plan = mp3g.Plan(s0, mode=mp3g.MODE_FAST, device=local)
+        for _ in range(3):
+            plan.execute(d_g, d_c, d_p, stream=h)
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(args.steps):
+            plan.execute(d_g, d_c, d_p, stream=h)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        ms = e0.elapsed_time(e1) / args.steps
+        plan.close()
+        hs = {"rewritten": 0, "zones": 0, "hot": 0}
+        if hasattr(mp3g.lib(), "mp3g_plan_hot_stats"):
+            cplan = mp3g.Plan(s0, mode=mp3g.MODE_FAST | mp3g.FLAG_HOT_STATS, device=local)
+            cplan.execute(d_g, d_c, d_p, stream=h)
+            hs = cplan.hot_stats()
+            cplan.close()
+        torch.cuda.synchronize(dev)
+        want, _ = oracle.dsp_streams(g2[:n_chk], c0[:n_chk], mp3g.streams_for([int(s0["n_granules"][0]),
+                                                                                int(s0["n_granules"][1])]))
+        got = d_p[:n_chk * 1152].cpu().numpy().reshape(-1, 576, 2)
+        out.append({"boost_db": 1.5 * b, "clipped_sample_fraction": round(float((np.abs(want) >= 32767).mean()), 5),
+                    "hot_fraction": round(hs["hot"] / n, 5), "rewritten_fraction": round(hs["rewritten"] / n, 5),
+                    "zones": hs["zones"], "kernel_ms": round(ms, 4), "max_dpcm_lsb": dpcm(got, want)})
+    return {"workload": f"c5 files x {copies} each, every granule's global_gain + boost (the same lines, a louder "
+                        f"master); reference peak about -6 dBFS", "granules": int(n), "rows": out}
+
+
 def hot_leg(args, rank, dev, stream, g, c, streams, local, d_c, fracs=(0.006, 0.06)):
     """the fast mode's magnitude bound.  Granules whose
     hybrid output exceeds it run again in the reference's operation order (the
@@ -979,6 +1035,10 @@ def main():
         hot_cliff = hot_leg(args, rank, dev, stream, g, c, streams, local, d_c,
                             fracs=tuple(float(x) for x in args.hot_fracs.split(",") if x))
 
+    real_loud = None
+    if args.config == "c3" and not args.no_hot and "fast" in res and rank == 0:
+        real_loud = real_loud_leg(args, rank, dev, stream, local)
+
     bitstream = None
     if not args.no_bitstream and args.config in ("c2", "c3"):
         bitstream = bitstream_leg(args.config, rank, dev, stream,
@@ -1074,6 +1134,8 @@ def main():
             out["modes"]["fast"]["hot_granules"] = hot_timed
         if hot_cliff is not None:
             out["modes"]["fast"]["hot_cliff"] = hot_cliff
+        if real_loud is not None:
+            out["modes"]["fast"]["real_loud"] = real_loud
         out["host_memory"] = host_mem
         if gather is not None:
             out["gather_ms"] = gather["ms"]
