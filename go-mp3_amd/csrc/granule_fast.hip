@@ -115,6 +115,9 @@ constexpr int kHist = 16;
 #endif
 constexpr int kSlots = kHist + 18;
 static_assert(kSlots == kFastRingSlots, "FastTables::sinfo indexes the staged ring");
+#ifndef MP3G_FAST_PCM_D16
+#define MP3G_FAST_PCM_D16 0  // (A/B) PCM as per-channel 16-bit stores instead of swap + merge
+#endif
 #ifndef MP3G_FAST_P43
 #define MP3G_FAST_P43 1  // long-block requantize through the p43 LDS table (0: arithmetic, A/B)
 #endif
@@ -1252,6 +1255,40 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
           pk[p] = __builtin_amdgcn_perm((uint32_t)(decltype(mono)::value ? r[0] : r[1]), (uint32_t)r[0], 0x05040100u);
         }
       };
+#if MP3G_FAST_PCM_D16
+      // (A/B) each lane stores its own channel's samples as 16-bit stores, no
+      // swap and no merge: per slot the wave writes 128 contiguous bytes; mono:
+      // the channel-0 lanes store (s, s) dwords, the others nothing
+      const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(
+          pcm + (size_t)g * 1152, (short)0, MP3G_PCM_BYTES_PER_GRANULE, 0x00020000);
+      if (nch == 2) {
+#pragma unroll
+        for (int p = 0; p < 9; p++) {
+          const int a = (int)__builtin_amdgcn_fmed3f(acc2[p].x, -32767.0f, 32767.0f);
+          const int b = (int)__builtin_amdgcn_fmed3f(acc2[p].y, -32767.0f, 32767.0f);
+          __builtin_amdgcn_raw_buffer_store_b16((unsigned short)a, rp, 4 * (32 * (2 * p) + k) + 2 * ch, 0, 2);
+          __builtin_amdgcn_raw_buffer_store_b16((unsigned short)b, rp, 4 * (32 * (2 * p + 1) + k) + 2 * ch, 0, 2);
+        }
+      } else {
+        const int off = ch ? kNoRecord : 0;
+#pragma unroll
+        for (int p = 0; p < 9; p++) {
+          const int a = (int)__builtin_amdgcn_fmed3f(acc2[p].x, -32767.0f, 32767.0f);
+          const int b = (int)__builtin_amdgcn_fmed3f(acc2[p].y, -32767.0f, 32767.0f);
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_perm((uint32_t)a, (uint32_t)a, 0x05040100u), rp,
+                                                off + 4 * (32 * (2 * p) + k), 0, 2);
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_perm((uint32_t)b, (uint32_t)b, 0x05040100u), rp,
+                                                off + 4 * (32 * (2 * p + 1) + k), 0, 2);
+        }
+      }
+    } else {
+      // as many stores as the output path, through a resource with no
+      // records: straight-line vmcnt accounting at the join
+      const __amdgpu_buffer_rsrc_t r0 = __builtin_amdgcn_make_buffer_rsrc(pcm, (short)0, 0, 0x00020000);
+#pragma unroll
+      for (int p = 0; p < 18; p++) __builtin_amdgcn_raw_buffer_store_b16((unsigned short)0, r0, 4 * p, 0, 2);
+    }
+#else
       if (nch == 2) pack(std::false_type{});
       else pack(std::true_type{});
       // stored right away: a store's data registers are free again once it
@@ -1265,6 +1302,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       for (int p = 0; p < 9; p++)
         __builtin_amdgcn_raw_buffer_store_b32(pk[p], rp, 4 * (32 * (2 * p + hi) + k), 0, 2);  // non-temporal: c2 -1.9 %, c3 -0.8 %
     }
+#endif
   };
 
   if constexpr (kStamp) {
