@@ -29,7 +29,7 @@ typedef struct mp3g_synth_params {
   int32_t mode;           // 0 stereo, 1 joint stereo, 2 dual channel, 3 mono
   int32_t bitrate_index;  // 9 = 128 kbps (MPEG-1); 8 = 64 kbps (MPEG-2)
   int32_t sfreq;          // 0 = 44.1 / 22.05 kHz
-  int32_t pad_;
+  int32_t gain_boost;     // added to every granule's global_gain (capped at 255): loud content
   double p_ms;            // joint stereo: P(mode_ext MS bit) per frame
   double p_is;            // joint stereo: P(mode_ext IS bit) per frame
   double p_event;         // P(a long -> start -> short.. -> stop run starts) per granule
@@ -180,7 +180,7 @@ struct Encoder {
                int16_t* lines) {
     const uint64_t start = w.pos;
     const bool shortblk = s->win_switch && s->block_type == 2;
-    s->global_gain = rng.range(140, 181);
+    s->global_gain = std::min(255, rng.range(140, 181) + P.gain_boost);
     s->scalefac_scale = rng.uni() < 0.2;
     s->preflag = !lsf && !shortblk && rng.uni() < 0.3;
     for (int k = 0; k < 3; k++) s->subblock_gain[k] = s->win_switch ? rng.range(0, 8) : 0;

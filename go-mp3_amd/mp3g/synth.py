@@ -200,7 +200,7 @@ def synth_pool_batch(n_streams, n_frames, seed=1, pool_frames=4096, **kw):
 # ---- synthetic bitstreams (libmp3gsynth.so, tooling) --------------------------
 class _SynthParams(C.Structure):
     _fields_ = [("seed", C.c_uint64), ("n_frames", C.c_int32), ("lsf", C.c_int32), ("mode", C.c_int32),
-                ("bitrate_index", C.c_int32), ("sfreq", C.c_int32), ("pad_", C.c_int32),
+                ("bitrate_index", C.c_int32), ("sfreq", C.c_int32), ("gain_boost", C.c_int32),
                 ("p_ms", C.c_double), ("p_is", C.c_double), ("p_event", C.c_double), ("p_mixed", C.c_double),
                 ("p_big", C.c_double), ("fill", C.c_double)]
 
@@ -219,14 +219,16 @@ def _synth():
 
 
 def encode_stream(seed, n_frames, mode=MODE_JOINT, lsf=False, bitrate_index=None, sfreq=0, p_ms=0.5, p_is=0.1,
-                  p_event=0.03, p_mixed=0.01, p_big=0.002, fill=0.9, expected=False):
+                  p_event=0.03, p_mixed=0.01, p_big=0.002, fill=0.9, expected=False, gain_boost=0):
     """A seeded Layer III bitstream: CBR frames (128 kbps MPEG-1 / 64 kbps MPEG-2
     by default) through the bit reservoir.  With expected=True also returns the
-    granule descriptors + coefficients a decoder must recover from it."""
+    granule descriptors + coefficients a decoder must recover from it.
+    gain_boost raises every granule's global_gain (loud content: +56 drives
+    the fast mode's hot-zone fallback)."""
     if bitrate_index is None:
         bitrate_index = 8 if lsf else 9
-    p = _SynthParams(seed, n_frames, int(lsf), mode, bitrate_index, sfreq, 0, p_ms, p_is, p_event, p_mixed,
-                     p_big, fill)
+    p = _SynthParams(seed, n_frames, int(lsf), mode, bitrate_index, sfreq, int(gain_boost), p_ms, p_is, p_event,
+                     p_mixed, p_big, fill)
     cap = n_frames * 1500 + 64
     out = np.zeros(cap, np.uint8)
     ng = n_frames * (1 if lsf else 2)

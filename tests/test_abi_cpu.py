@@ -6,6 +6,8 @@ import os
 import re
 import subprocess
 
+import ctypes as C
+
 import numpy as np
 import pytest
 
@@ -114,6 +116,23 @@ def test_no_cpu_fallback_without_gpu():
     with pytest.raises(mp3g.Mp3gError) as e:
         mp3g.decode_host(g, c, s)
     assert e.value.status in (3, 4)
+
+
+def test_clock_probe_checks_arguments_before_the_device():
+    """mp3g_debug_clock_probe (diagnostic) refuses null buffers, 0 or > 1024
+    probes and a max_ms outside 1..10,000 with MP3G_ERR_INVALID_ARGUMENT,
+    before it touches a device; the binding checks the output size."""
+    L = mp3g.lib()
+    buf = C.c_void_p(0x1000)  # never dereferenced: the arguments fail first
+    assert L.mp3g_debug_clock_probe(0, None, buf, 8, 10, None) == 1
+    assert L.mp3g_debug_clock_probe(0, buf, None, 8, 10, None) == 1
+    assert L.mp3g_debug_clock_probe(0, buf, buf, 0, 10, None) == 1
+    assert L.mp3g_debug_clock_probe(0, buf, buf, 1025, 10, None) == 1
+    assert L.mp3g_debug_clock_probe(0, buf, buf, 8, 0, None) == 1
+    assert L.mp3g_debug_clock_probe(0, buf, buf, 8, 10001, None) == 1
+    import torch
+    with pytest.raises(ValueError):
+        mp3g.clock_probe(torch.zeros(1, dtype=torch.int32), torch.zeros(4, dtype=torch.int64), 1, 10)
 
 
 def test_exact_kernel_has_no_fma():

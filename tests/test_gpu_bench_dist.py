@@ -85,3 +85,28 @@ def test_bench_one_rank_rccl():
     assert d["gather"]["backend"].startswith("RCCL") and d["gather"]["bytes"] == 20000 * 2304
     assert d["gather"]["parity"]["max_dpcm_lsb"] <= 1
     assert d["max_dpcm_lsb"] <= 1
+
+
+def test_bench_pinned_budget_guard():
+    """bench.py's pinned-memory budget per rank: with a
+    budget too small for the bitstream leg's pinned buffers, the PCIe pass
+    and the pipelined drop-in are skipped and say so, the device leg and its
+    oracle parity still run, and 2 gloo ranks gather into pageable memory."""
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--config", "c2", "--backend", "gloo", "--single-mode", "--no-polyphase", "--no-hot"]
+    env = dict(os.environ, OMP_NUM_THREADS="4", MP3G_BENCH_PINNED_GB="0.01")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=REPO, env=env)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert r.returncode == 0 and len(lines) == 1, r.stdout[-3000:] + r.stderr[-5000:]
+    d = json.loads(lines[0])
+    hm = d["host_memory"]
+    legs = {x["leg"] for x in hm["skipped_legs"]}
+    assert "bitstream PCIe pass + pipelined drop-in" in legs, hm
+    assert any(x.startswith("gloo gather") for x in legs), hm
+    assert hm["peak_pinned_gb_by_bench_max_over_ranks"] <= 0.011
+    b = d["bitstream"]
+    assert b["end_to_end"]["skipped"] and b["end_to_end"]["pipelined_s"] is None and b["decoder_api"] is None
+    assert b["huffman_plus_dsp_ms"] > 0 and b["max_dpcm_lsb_vs_oracle"] <= 1
+    assert d["gather"]["parity"]["max_dpcm_lsb"] <= 1

@@ -190,6 +190,44 @@ def test_decode_streams_into_fast_concurrent(gpu, sample_files):
         assert np.array_equal(pcm, want), key
 
 
+def test_decode_streams_into_fast_loud_zone_growth(gpu):
+    """The pipelined drop-in's zone scratch (the fast kernel's deferred hot
+    zones) is sized by each group's chunk count and grown on demand: streams
+    that get longer group after group, some of them loud (every granule's
+    global_gain + 56: hot zones everywhere), in fast mode at 1, 4 and the
+    automatic number of groups -- every stream within 1 LSB of the oracle's
+    NewDecoder + ReadAll of the same bytes, with its end status, and the
+    pipelined PCM equal to the whole-batch plan's."""
+    import torch
+    from mp3g import synth
+    datas = [synth.encode_stream(301 + k, 8 + 40 * k, gain_boost=56 if k % 3 == 1 else 0, p_event=0.1,
+                                 p_mixed=0.1) for k in range(8)]
+    want, ws, wst = gpu.decode_streams(datas, mode=gpu.MODE_FAST)
+    n_all = int(sum(int(x["n_granules"]) for x in ws))
+    for n_groups in (1, 4, 0):
+        out = torch.full((n_all * 1152,), 0x5A5A, dtype=torch.int16).pin_memory()
+        n, s, st = gpu.decode_streams_into(datas, out, mode=gpu.MODE_FAST, n_groups=n_groups)
+        assert n == n_all and list(st) == list(wst), n_groups
+        pcm = out.numpy().reshape(-1, 576, 2)
+        assert np.array_equal(pcm, want), n_groups
+    gpu.lib().mp3g_release_cached_buffers()
+    for k, d in enumerate(datas):
+        ost, opcm = oracle.decode_all(d)
+        lo, m = int(ws[k]["first_granule"]), int(ws[k]["n_granules"])
+        ref = np.frombuffer(opcm, np.int16).reshape(-1, 576, 2)
+        assert ost == oracle.ORC_OK and len(ref) == m, k
+        assert int(np.abs(want[lo:lo + m].astype(np.int32) - ref).max()) <= 1, k
+    # the loud streams do take the fallback (hot granules, counted by the plan build)
+    g, c, s, _ = gpu.parse_streams([datas[1]], n_threads=1)
+    dev = torch.device("cuda:0")
+    plan = gpu.Plan(s, mode=gpu.MODE_FAST | gpu.FLAG_HOT_STATS)
+    d_p = torch.empty(len(g) * 1152, dtype=torch.int16, device=dev)
+    plan.execute(torch.from_numpy(g.view(np.uint8).copy()).to(dev),
+                 torch.from_numpy(c.reshape(-1).copy()).to(dev), d_p)
+    assert plan.hot_stats()["hot"] > 0
+    plan.close()
+
+
 def test_decode_streams_into_buffer_kinds(gpu):
     """The PCM copy-out of mp3g_decode_streams_into takes the library's copy
     kernel into a pinned, 16-B aligned buffer (through its device address,
