@@ -153,6 +153,19 @@ std::vector<uint64_t> spread_chunks(const mp3g_stream* streams, uint32_t n_strea
 // model's 3,334 chunks put 4 workgroups on 66 CUs and 3 on the others, and
 // the 4-workgroup CUs set the launch time) and the streams are cut into
 // chunks of equal length.
+//
+// Whole rounds (round 6): the number of rounds R is then chosen on the plans
+// it actually yields -- R x resident chunks spread over the streams, the
+// longest chunk k_R -- at cost (R + tail) (k_R + 4): 4 granule-steps of
+// per-chunk overhead (the two-granule halo and the prologue; fitted to the
+// c3 chunk sweep, tools/chunk_sweep.sh: 7.90 / 7.67 / 7.60 / 7.79 M cycles at
+// 8 / 4 / 2 / 1 rounds) and a tail of MP3G_CHUNK_TAIL rounds, far below the
+// 0.5 round of the fractional model (equal chunks in whole rounds end
+// together).  c3: 8 -> 4 rounds of 128 granules (-1.4 % in time at the clock
+// the chip then holds); c2 stays one round.
+#ifndef MP3G_CHUNK_TAIL
+#define MP3G_CHUNK_TAIL 0.15
+#endif
 std::vector<uint64_t> auto_chunks(const mp3g_stream* streams, uint32_t n_streams, int device, uint32_t mode) {
   const uint64_t k = auto_chunk(streams, n_streams, device, mode);
   uint64_t c0 = 0;
@@ -166,8 +179,23 @@ std::vector<uint64_t> auto_chunks(const mp3g_stream* streams, uint32_t n_streams
     for (uint32_t s = 0; s < n_streams; s++) c[s] = (streams[s].n_granules + k - 1) / k;
     return c;
   }
-  const uint64_t rounds = (c0 + resident - 1) / resident;
-  return spread_chunks(streams, n_streams, rounds * resident);
+  const uint64_t r0 = (c0 + resident - 1) / resident;
+  if (MP3G_CHUNK_TAIL <= 0.0) return spread_chunks(streams, n_streams, r0 * resident);
+  // candidates: the fractional model's R and every R below it down to 1
+  uint64_t best_r = r0;
+  double best = 0.0;
+  for (uint64_t r = r0; r >= 1; r--) {
+    const std::vector<uint64_t> c = spread_chunks(streams, n_streams, r * resident);
+    uint64_t kr = 0;
+    for (uint32_t s = 0; s < n_streams; s++)
+      if (c[s]) kr = std::max<uint64_t>(kr, (streams[s].n_granules + c[s] - 1) / c[s]);
+    const double cost = ((double)r + MP3G_CHUNK_TAIL) * (double)(kr + 4);
+    if (best == 0.0 || cost < best) {
+      best = cost;
+      best_r = r;
+    }
+  }
+  return spread_chunks(streams, n_streams, best_r * resident);
 }
 
 }  // namespace
