@@ -1877,22 +1877,36 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
     uint32_t* const zone_count = aux;
     ChunkDesc* const zone_list = reinterpret_cast<ChunkDesc*>(aux + 8);
     const uint32_t zone_cap = __builtin_amdgcn_readfirstlane(aux[2]);
+    // every zone as pieces of at most kZonePiece granules (kernels.h), one
+    // atomic for all of them
+    uint32_t n_pieces = 0;
+    for (uint32_t i = 0; i < nz; i++) {
+      const uint32_t zs = __builtin_amdgcn_readfirstlane(s.zone[i][0]), ze = __builtin_amdgcn_readfirstlane(s.zone[i][1]);
+      n_pieces += (ze - zs + kZonePiece - 1) / kZonePiece;
+    }
     uint32_t base = 0;
-    if (lane_fresh() == 0) base = atomicAdd(zone_count, nz);
+    if (lane_fresh() == 0) base = atomicAdd(zone_count, n_pieces);
     base = __builtin_amdgcn_readfirstlane(base);  // lane 0 is the first active lane
-    const int zl = lane_fresh();
-    if ((uint32_t)zl < nz && base + (uint32_t)zl < zone_cap) {  // (always below the capacity: see kZones)
-      const uint32_t zs = s.zone[zl][0], ze = s.zone[zl][1];
-      ChunkDesc z;
-      z.out_first = zs;
-      z.stream_first = cd.stream_first;
-      z.n_out = ze - zs;
-      z.stream = cd.stream;
-      // entry state as the chunk's; the exported state when the zone ends
-      // the chunk (it then overwrites this pass's export)
-      z.flags = (cd.flags & kChunkStateIn) | (ze == end ? (cd.flags & kChunkStateOut) : 0u);
-      z.reserved = 0;
-      zone_list[base + zl] = z;
+    for (uint32_t i = 0; i < nz; i++) {
+      const uint32_t zs = __builtin_amdgcn_readfirstlane(s.zone[i][0]), ze = __builtin_amdgcn_readfirstlane(s.zone[i][1]);
+      const uint32_t np = (ze - zs + kZonePiece - 1) / kZonePiece;
+      const uint32_t l = (uint32_t)lane_fresh();
+      // (always below the capacity: zone_list_capacity counts every piece)
+      if (l < np && base + l < zone_cap) {
+        const uint32_t ps = zs + l * kZonePiece, pe = min(ps + kZonePiece, ze);
+        ChunkDesc z;
+        z.out_first = ps;
+        z.stream_first = cd.stream_first;
+        z.n_out = pe - ps;
+        z.stream = cd.stream;
+        // entry state as the chunk's (the zone launch replays the piece's halo
+        // from it or from zero, as for any chunk); the exported state when
+        // the piece ends the chunk (it then overwrites this pass's export)
+        z.flags = (cd.flags & kChunkStateIn) | (pe == end ? (cd.flags & kChunkStateOut) : 0u);
+        z.reserved = 0;
+        zone_list[base + l] = z;
+      }
+      base += np;
     }
   }
   // (counting build) a chunk counts its flagged granules even when none of

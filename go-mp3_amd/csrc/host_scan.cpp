@@ -689,12 +689,12 @@ int mp3g_decode_streams_into(int device, uint32_t n_streams, const uint8_t* cons
         break;
       }
       if (!chunks.empty()) std::memcpy(h_chunks, chunks.data(), chunks.size() * sizeof(ChunkDesc));
-      // the fast kernel's zone scratch: kZoneListPerChunk zones per chunk of
-      // this group's plan (the cost model keeps chunks far fewer than
-      // granules), grown on demand -- after the kernels that use the old one
+      // the fast kernel's zone scratch: the pieces of kZoneListPerChunk zones
+      // per chunk of this group's plan (zone_list_capacity: the cost model
+      // keeps chunks far fewer than granules), grown on demand -- after the kernels that use the old one
       // are done (the scratch is shared by every group on `comp`)
       if ((mode & 0xffu) == MP3G_MODE_FAST) {
-        const uint64_t zone_cap = (uint64_t)kZoneListPerChunk * std::max<uint64_t>(8, chunks.size());
+        const uint64_t zone_cap = zone_list_capacity(chunks.data(), chunks.size());
         if (zone_cap > 0xffffffffu) {
           rc = abi_fail(MP3G_ERR_UNSUPPORTED, "decode_streams_into: group too large");
           break;

@@ -40,8 +40,9 @@ constexpr int kVariantExact4 = 4;
 // hybrid output -- to the list as chunks of their own, counting them; a
 // second launch (the exact v4 kernel over the list) decodes them in the
 // reference's order and, when its last workgroup is done, empties the list
-// for the next launch.  kZoneListPerChunk zones per chunk (the fast kernel's
-// own limit) never overflow it, and launch_fast refuses a smaller list (the
+// for the next launch.  zone_list_capacity entries (the pieces of the
+// kZoneListPerChunk zones a chunk records at most) never overflow it, and
+// launch_fast refuses a list of fewer than kZoneListPerChunk per chunk (the
 // production kernel has no in-wave fallback).  Device memory of the plan (or pipeline) that
 // owns it, laid out as
 //   uint32 [0] zones listed, [1] zone-launch workgroups done, [2] capacity,
@@ -49,6 +50,22 @@ constexpr int kVariantExact4 = 4;
 // (zone_scratch_init writes a fresh one); launches that share it must be
 // stream-ordered.
 constexpr uint32_t kZoneListPerChunk = 8;
+// A zone goes into the list in pieces of at most kZonePiece granules (round
+// 6): each piece replays its own two-granule halo in the zone launch, whose
+// waves then take short pieces instead of one long zone serially (with
+// 128-granule chunks a saturated chunk's last zone runs to the chunk end).
+#ifndef MP3G_ZONE_PIECE
+#define MP3G_ZONE_PIECE 16
+#endif
+constexpr uint32_t kZonePiece = MP3G_ZONE_PIECE;
+// The list entries a chunk can need: its <= kZoneListPerChunk zones lie in
+// its output range, so their pieces number at most ceil(n_out / kZonePiece)
+// + kZoneListPerChunk.
+inline uint64_t zone_list_capacity(const ChunkDesc* c, size_t n) {
+  uint64_t cap = 0;
+  for (size_t i = 0; i < n; i++) cap += kZoneListPerChunk + (c[i].n_out + kZonePiece - 1) / kZonePiece;
+  return cap < 64 ? 64 : cap;
+}
 struct ZoneScratch {
   uint32_t* aux;  // the header above; the list at aux + 8
   uint32_t cap;

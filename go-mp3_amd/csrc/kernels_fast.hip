@@ -33,7 +33,11 @@ __device__ float g_req[4][8207];
 #include "granule_wexact.hip"
 
 #ifndef MP3G_ZONE_CHUNKS_PER_WG
-#define MP3G_ZONE_CHUNKS_PER_WG 64  // zone-launch workgroups: one per this many chunks (16 .. 512)
+// zone-launch workgroups: one per this many chunks (16 .. 512).  32 since the
+// round-6 chunk model halved c3's chunk count (128 granules per chunk): c3
+// keeps its 512 workgroups (at 256 the ~10 %-hot batch took 8.2 ms instead of
+// 6.3), c2 gets 128
+#define MP3G_ZONE_CHUNKS_PER_WG 32
 #endif
 
 namespace mp3g {
@@ -76,9 +80,9 @@ hipError_t launch_fast(const ChunkDesc* d_chunks, uint32_t n_chunks, const mp3g_
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !zones || d_stamps) return e;
   // the zone launch: the exact v4 kernel over the list, its waves taking zone
-  // after zone; one workgroup of 8 waves per 64 chunks of the launch, at most
-  // two per CU (an empty list ends every workgroup at once: the fewer, the
-  // cheaper -- c2's 4,096 chunks get 64)
+  // after zone; one workgroup of 8 waves per MP3G_ZONE_CHUNKS_PER_WG chunks of
+  // the launch, at most two per CU (an empty list ends every workgroup at
+  // once: the fewer, the cheaper -- c2's 4,096 chunks get 128)
   const uint32_t blocks = std::max(16u, std::min<uint32_t>(n_chunks / MP3G_ZONE_CHUNKS_PER_WG, 512u));
   hipLaunchKernelGGL(v4::granule_wexact_kernel<true>, dim3(blocks), dim3(64 * v4::kXWaves), 0, stream,
                      reinterpret_cast<const ChunkDesc*>(aux + 8), zones->cap, d_gran, d_coef, d_state_in,

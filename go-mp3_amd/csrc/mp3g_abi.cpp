@@ -401,7 +401,7 @@ int mp3g_plan_create(int device, const mp3g_stream* streams, uint32_t n_streams,
   // can record per chunk: the list never overflows)
   const size_t tb = (p->chunks.size() * sizeof(ChunkDesc) + 255) & ~(size_t)255;
   const bool fast = plan_variant(mode) == kVariantFast;
-  const uint64_t zone_cap = fast ? (uint64_t)kZoneListPerChunk * std::max<size_t>(8, p->chunks.size()) : 0u;
+  const uint64_t zone_cap = fast ? zone_list_capacity(p->chunks.data(), p->chunks.size()) : 0u;
   if (zone_cap > 0xffffffffu) {
     delete p;
     return fail(MP3G_ERR_UNSUPPORTED, "fast-mode plan of more than 2^29 chunks");
