@@ -44,7 +44,8 @@ extern "C" {
  *    mp3g_huffman_stage_flags.
  * 5: mp3g_plan_hot_stats and MP3G_FLAG_HOT_STATS (the fast kernel's
  *    hot-granule fallback counters); a fast-mode plan owns a zone list its
- *    launches share, so executions of one plan must be stream-ordered. */
+ *    launches share, so executions of one plan must be stream-ordered.
+ *    (Compatible additions since: the diagnostic mp3g_debug_clock_probe.) */
 #define MP3G_ABI_VERSION 5
 
 /* ---- status codes ------------------------------------------------------ */
