@@ -101,7 +101,18 @@ def max_over_ranks(value, device=None):
     return float(t.item())
 
 
-def gather_pcm(pcm, dst=0, out=None):
+# Largest single point-to-point message of gather_pcm: a rank's c4 slice is
+# 4.83 GB (2^32 + bytes, more than a 32-bit element count), so every transfer
+# goes as pieces of at most this many bytes, matched in order on both sides
+# (RCCL and gloo keep the order of messages between one pair of ranks).
+GATHER_PIECE_BYTES = 1 << 30
+
+
+def _pieces(n, piece):
+    return [(a, min(a + piece, n)) for a in range(0, n, piece)]
+
+
+def gather_pcm(pcm, dst=0, out=None, piece_bytes=None):
     """Gather every rank's PCM (a 1-D tensor of any dtype, sizes may differ) to
     `dst`: returns `out` -- the concatenation in rank order, as raw bytes
     viewed as pcm's dtype -- on dst, None elsewhere.
@@ -112,7 +123,8 @@ def gather_pcm(pcm, dst=0, out=None):
     its own part into place.  No per-rank staging buffers and no concatenation
     copy: at c4 that is 38.65 GB written once on rank 0.  xGMI
     is point-to-point, so the world - 1 transfers run concurrently on rank 0's
-    links.  Works on GPU tensors under RCCL and on CPU tensors under gloo.
+    links, each in pieces of at most GATHER_PIECE_BYTES (piece_bytes
+    overrides).  Works on GPU tensors under RCCL and on CPU tensors under gloo.
     """
     import torch
     import torch.distributed as dist
@@ -126,9 +138,11 @@ def gather_pcm(pcm, dst=0, out=None):
     sizes = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(sizes, n)
     sizes = [int(s.item()) for s in sizes]
+    piece = int(piece_bytes or GATHER_PIECE_BYTES)
     if rank != dst:
         if flat.numel():
-            for req in dist.batch_isend_irecv([dist.P2POp(dist.isend, flat, dst)]):
+            ops = [dist.P2POp(dist.isend, flat[a:b], dst) for a, b in _pieces(flat.numel(), piece)]
+            for req in dist.batch_isend_irecv(ops):
                 req.wait()
         return None
     total = sum(sizes)
@@ -141,8 +155,8 @@ def gather_pcm(pcm, dst=0, out=None):
                              f"need {total} B on {flat.device}")
         out_b = out_b[:total]
     offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
-    ops = [dist.P2POp(dist.irecv, out_b[int(offs[r]):int(offs[r + 1])], r)
-           for r in range(world) if r != dst and sizes[r]]
+    ops = [dist.P2POp(dist.irecv, out_b[int(offs[r]) + a:int(offs[r]) + b], r)
+           for r in range(world) if r != dst and sizes[r] for a, b in _pieces(sizes[r], piece)]
     reqs = dist.batch_isend_irecv(ops) if ops else []
     out_b[int(offs[dst]):int(offs[dst + 1])].copy_(flat)
     for req in reqs:

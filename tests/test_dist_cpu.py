@@ -68,14 +68,18 @@ def _worker(rank, world, port, q):
         # the tail stays untouched)
         pre = torch.full((len(g) * 1152 + 99,), 7, dtype=torch.int16) if rank == 0 else None
         out2 = mdist.gather_pcm(mine, out=pre)
+        # and in small pieces (each rank's slice as several messages matched
+        # in order: the 1-GiB pieces of a c4 slice, scaled down)
+        out3 = mdist.gather_pcm(mine, piece_bytes=1000)
         if rank == 0:
             want, _ = oracle.dsp_streams(g, c, s)
             same = np.array_equal(out.numpy().reshape(-1, 576, 2), want)
             same2 = out2 is pre and np.array_equal(pre[:len(g) * 1152].numpy().reshape(-1, 576, 2), want) \
                 and bool((pre[len(g) * 1152:] == 7).all())
-            q.put(("ok", t, bool(same and same2)))
+            same3 = np.array_equal(out3.numpy().reshape(-1, 576, 2), want)
+            q.put(("ok", t, bool(same and same2 and same3)))
         else:
-            assert out is None and out2 is None
+            assert out is None and out2 is None and out3 is None
         dist.barrier()
     finally:
         dist.destroy_process_group()
