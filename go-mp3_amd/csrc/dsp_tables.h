@@ -67,6 +67,12 @@ void build_tables(DspTables* t);
 //   dwin[i][j] (a_i = 16+i | 48-i, b_i = 16-i | i-16).
 // slots per ring column of the fast kernel (granule_fast.hip kSlots)
 constexpr int kFastRingSlots = 34;
+// entries of the fast kernel's |x|^(4/3) table (MP3G_FAST_P43_N: 256 = |x| < 128)
+#ifndef MP3G_FAST_P43_N
+#define MP3G_FAST_P43_N 256
+#endif
+constexpr int kFastP43 = MP3G_FAST_P43_N;
+static_assert(kFastP43 == 256 || kFastP43 == 512, "p43 table size");
 struct FastTables {
   float c36[18][18];   // distinct cosN36 columns (= DspTables::cos36_distinct)
   float cos12[6][12];
@@ -101,9 +107,9 @@ struct FastTables {
   uint16_t sfb_long[kCombos][23];
   uint16_t sfb_short[kCombos][14];
   int8_t pretab[22];
-  // the fast kernel's long-block requantize: p43[x + 128] = sign(x) |x|^(4/3)
-  // as float32 (= +-req[0][|x|]) for x = -128..127
-  float p43[256];
+  // the fast kernel's long-block requantize: p43[x + kFastP43 / 2] = sign(x) |x|^(4/3)
+  // as float32 (= +-req[0][|x|]) for x = -kFastP43 / 2 .. kFastP43 / 2 - 1
+  float p43[kFastP43];
 };
 void build_fast_tables(const DspTables& t, FastTables* f);
 

@@ -155,7 +155,7 @@ struct __align__(16) SharedSmem {
   __device__ uint32_t lband_at(int c, int k) const { return lbd[c][k].x; }
   // FastTables::p43: sign(x) |x|^(4/3) of x = -128..127 at byte offset
   // 4 x + 512 -- the long-block requantize is a table read and one multiply
-  float p43[256];
+  float p43[kFastP43];
 };
 // per-wave working set 9.1 KB.  The workgroup (8 waves + shared tables) must
 // stay <= 64 x 1280 B (gfx950 LDS allocation granule) for 2 workgroups
@@ -172,7 +172,9 @@ struct __align__(16) WaveSmem {
   // the parse's guarantee, maindata/huffman.go:127-134, so they are neither
   // read here nor written by the main-data kernel, MP3G_HUFF_ROWS_COUNT1;
   // c3 -0.4 % against whole rows, tools/gpu_r03z.sh)
+#if !MP3G_FAST_DESC_VGPR
   mp3g_granule descn;
+#endif
   // requantization exponents n4 / 4 (float16, exact) of the long bands
   // [ch][sfb] and short bands [ch][sfb][win]; in the fast loop's all-long
   // granules the long bands' gains 2^(n4 / 4) as float32 [ch][sfb] instead
@@ -1122,7 +1124,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
       for (int i = 1; i <= 8; i++) d |= ((lb >> (5 + 2 * i)) & 1u) * (15u << (4 * (i - 1)));
       (&sh.lbd[0][0])[e] = make_uint2(lb, d);
     }
-    for (int e = t; e < 256; e += kLanes * kWaves) sh.p43[e] = g_fast.p43[e];
+    for (int e = t; e < kFastP43; e += kLanes * kWaves) sh.p43[e] = g_fast.p43[e];
   };
   const int lane = threadIdx.x & (kLanes - 1);
   // wave-uniform in an SGPR: the chunk descriptor then comes in by scalar
@@ -1447,7 +1449,7 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
         // (v_pk_mad_u16 by hand: the compiler splits it into a shift and an
         // add; op_sel_hi 0 on the inline constant: its high half would be 0)
         uint32_t t;
-        asm("v_pk_mad_u16 %0, %1, 4, %2 op_sel_hi:[1,0,1]" : "=v"(t) : "v"(cw[q]), "s"(0x02000200u));
+        asm("v_pk_mad_u16 %0, %1, 4, %2 op_sel_hi:[1,0,1]" : "=v"(t) : "v"(cw[q]), "s"(0x00010001u * 2u * kFastP43));
         big |= t;
         x[2 * q] = *reinterpret_cast<const float*>(tb + (t & 0xffffu));
         x[2 * q + 1] = *reinterpret_cast<const float*>(tb + (t >> 16));
@@ -1457,7 +1459,8 @@ granule_fast_kernel(const ChunkDesc* __restrict__ chunks, uint32_t n_chunks, con
 #endif
 #pragma unroll
       for (int j = 0; j < 18; j++) x[j] *= gq[j >> 1];
-      if (big & 0xfc00fc00u) {
+      // (an offset at or past the table's 4 kFastP43 bytes: some |x| >= kFastP43 / 2)
+      if (big & (0x00010001u * (0x10000u - 4u * kFastP43))) {
 #pragma unroll
         for (int q = 0; q < 9; q++) {
           x[2 * q] = requant_gain(cw[q] & 0xffffu, gq[q]);

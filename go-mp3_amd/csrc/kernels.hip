@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <new>
 
 #include "../../include/mp3g.h"
 #include "dsp_tables.h"
@@ -32,9 +33,12 @@ namespace mp3g {
 hipError_t upload_tables(const DspTables& tables) {
   hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_tab), &tables, sizeof(DspTables), 0, hipMemcpyHostToDevice);
   if (e != hipSuccess) return e;
-  FastTables fast;
-  build_fast_tables(tables, &fast);
-  e = upload_fast_tables(fast, &tables.req[0][0]);
+  // (54 KB: on the heap, not on the stack of whichever thread first uses the device)
+  FastTables* fast = new (std::nothrow) FastTables;
+  if (!fast) return hipErrorOutOfMemory;
+  build_fast_tables(tables, fast);
+  e = upload_fast_tables(*fast, &tables.req[0][0]);
+  delete fast;
   if (e != hipSuccess) return e;
   HuffLut* lut = new HuffLut;
   if (!build_huff_lut(lut)) {

@@ -16,7 +16,7 @@ vobjs=""
 for TU in $TUS; do
   EXTRA=""; [ "$TU" = kernels_fast.hip ] && EXTRA="-mllvm -disable-machine-licm -mllvm -misched-cluster=0"
   $HIPCC $CXXFLAGS $EXTRA $FLAGS -c "$C/$TU" -o "$B/$TU.o"
-  objs=$(echo "$objs" | grep -v "/$TU.o")
+  objs=$(echo "$objs" | grep -v "/$TU.o" || true)
   vobjs="$vobjs $B/$TU.o"
 done
 $HIPCC --offload-arch=gfx950 -shared -o "$C/../mp3g/libmp3g_$TAG.so" $objs $vobjs
