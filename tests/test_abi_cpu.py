@@ -233,3 +233,22 @@ def test_fast_mode_bounds_match_the_kernel():
     s = float(re.search(r"#define MP3G_HOT_S ([0-9.]+)f", src).group(1))
     l1 = float(re.search(r"#define MP3G_HOT_L1 ([0-9.]+)f", src).group(1))
     assert (s, l1) == (mp3g.FAST_HOT_S, mp3g.FAST_HOT_L1)
+
+
+def test_c_consumer_builds_and_fails_loudly_without_a_gpu(tmp_path):
+    """examples/mp3g_decode.c compiles as C99 against include/mp3g.h alone and
+    links libmp3g.so; with no gfx950 device it exits 1 with the library's
+    status text instead of decoding anything on the CPU."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present: tests/test_gpu_c_example.py runs it")
+    exe = str(tmp_path / "mp3g_decode")
+    subprocess.check_call(["gcc", "-std=c99", "-O2", "-Wall", "-Wextra", "-Werror", "-I",
+                           os.path.join(REPO, "include"), os.path.join(REPO, "examples", "mp3g_decode.c"),
+                           "-L", os.path.join(REPO, "go-mp3_amd", "mp3g"), "-lmp3g",
+                           "-Wl,-rpath," + os.path.join(REPO, "go-mp3_amd", "mp3g"), "-o", exe])
+    out = tmp_path / "o.pcm"
+    r = subprocess.run([exe, os.path.join(REPO, "tests", "golden", "classic_lame.mp3"), str(out)],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and "no gfx950 device" in r.stderr
+    assert out.read_bytes() == b""
